@@ -1,0 +1,248 @@
+"""Benchmark of the detection-output hot path (BASELINE.json metric, configs[1] / configs[2]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model ssd|frcnn|both] [--no-cpu]
+
+A step = one forward of the detector over one batch of synthetic 640x640 images already resident in
+HBM (preprocess -> backbone -> heads -> decode -> NMS -> final top-k), replayed from a captured
+hipGraph.  N=1 workload: SSDLite320-MobileNetV3 at batch 32 (configs[1]); FRCNN-R50-FPN-v2 at
+batch 8 (configs[2]) is measured beside it and reported under "frcnn".  For N>1 the script is
+launched by torch.distributed.run: one process per GPU, each replays its own batch (weak scaling:
+images are independent, no collective on the data path); the timed region is bracketed by a
+barrier + device sync and the max over ranks is taken.
+
+Extra objects on the JSON line:
+  roofline      the dominant kernel of the SSD step (by measured time): algorithmic bytes or flops
+                per launch / its average launch time (HIP events on the plan's stream)
+  cpu_baseline  the CPU oracle (a restatement of the reference's torchvision CPU path, detect.py's
+                batch=1 loop) timed on a bounded sample on this host, rank 0 only
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3   # dense fp32 MFMA (= fp32 vector peak)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+        return dist, dist.get_rank(), world
+    torch.cuda.set_device(0)
+    return None, 0, 1
+
+
+def timed_steps(plan, stream, steps, warmup, dist):
+    for _ in range(warmup):
+        plan.replay(stream)
+    stream.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.replay(stream)
+    stream.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+# ------------------------------------------------------------------------------ per-op costs
+def op_work(op):
+    """(kind, algorithmic flops, algorithmic HBM bytes) of one plan op (None if not modelled)."""
+    from edgeml_amd import ops as O
+    i = op.i
+    if op.kind == O.CONV:
+        B, H, W, Cin, Ho, Wo, Cout, KH, KW = (i[k] for k in range(9))
+        M = B * Ho * Wo
+        flops = 2.0 * M * Cout * KH * KW * Cin
+        byts = 4.0 * (B * H * W * Cin + Cout * KH * KW * Cin + M * Cout)
+        if op.p.get(4) is not None:
+            byts += 4.0 * M * Cout
+        return "conv", flops, byts
+    if op.kind == O.DWCONV:
+        B, H, W, C, Ho, Wo, K = (i[k] for k in range(7))
+        return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
+    return None
+
+
+def per_op_times(plan, stream, reps=20):
+    """Average device time of each op of the plan, run alone between HIP events on `stream`."""
+    import ctypes
+    from edgeml_amd import ops as O
+    L = O.lib()
+    res = []
+    recs = plan.records
+    sh = O.stream_handle(stream)
+    with torch.cuda.stream(stream):
+        for k in range(len(recs)):
+            ptr = recs[k:k + 1].ctypes.data_as(ctypes.c_void_p)
+            O.check(L.edgedet_plan_run(ptr, 1, sh))
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                L.edgedet_plan_run(ptr, 1, sh)
+            e1.record(stream)
+            e1.synchronize()
+            res.append(e0.elapsed_time(e1) / reps)
+    return res
+
+
+def roofline_for(plan, stream, step_ms):
+    """Pick the kernel family that dominates the step and price its largest launch."""
+    times = per_op_times(plan, stream)
+    fam = {}
+    for op, t in zip(plan.ops, times):
+        w = op_work(op)
+        name = w[0] if w else f"kind{op.kind}"
+        fam[name] = fam.get(name, 0.0) + t
+    dom = max(fam, key=fam.get)
+    best = None
+    for op, t in zip(plan.ops, times):
+        w = op_work(op)
+        if w and w[0] == dom and (best is None or t > best[1]):
+            best = (op, t, w)
+    breakdown = {k: round(v, 4) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])}
+    if best is None:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": dom, "family_ms": breakdown}
+    op, t, (name, flops, byts) = best
+    if name == "conv":
+        ach = flops / (t * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFS, 4), "traffic": None, "kernel": "conv_mfma_kernel",
+                "launch": op.name, "launch_ms": round(t, 4), "algorithmic_flops": flops,
+                "family_ms": breakdown, "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
+    ach = byts / (t * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": name, "launch": op.name,
+            "launch_ms": round(t, 4), "algorithmic_bytes": byts, "family_ms": breakdown,
+            "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def cpu_baseline(kind, budget_s=15.0):
+    """The CPU oracle (restated reference path) on a bounded sample, batch=1 like detect.py."""
+    from edgeml_amd import synthetic
+    from oracle.frcnn import FasterRCNNOracle
+    from oracle.ssdlite import SSDLiteOracle
+    torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    if kind == "ssd":
+        m = SSDLiteOracle(synthetic.synthetic_state_dict("ssd", 91, True), 91, True)
+    else:
+        m = FasterRCNNOracle(synthetic.synthetic_state_dict("faster_rcnn", 91), 91)
+    n, t0 = 0, time.perf_counter()
+    m(list(synthetic.make_batch(1, 640, 640, seed=999)))  # warm-up
+    t0 = time.perf_counter()
+    while True:
+        m(list(synthetic.make_batch(1, 640, 640, seed=1000 + n)))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} synthetic 640x640 images, batch=1 ({el:.1f}s), {kind} CPU oracle "
+                      f"(PyTorch-CPU + C restatement of the torchvision eval path)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="both", choices=["ssd", "frcnn", "both"])
+    ap.add_argument("--ssd-batch", type=int, default=32)
+    ap.add_argument("--frcnn-batch", type=int, default=8)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    dist, rank, world = dist_setup(args.gpus)
+    from edgeml_amd import models, synthetic
+    stream = torch.cuda.Stream()
+    out = {}
+    if args.model in ("ssd", "both"):
+        B = args.ssd_batch
+        m = models.ssdlite320_mobilenet_v3_large().to("cuda")
+        plan = m.plan(B, 640, 640)
+        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank).cuda())
+        plan.capture(stream)
+        el = timed_steps(plan, stream, args.steps, args.warmup, dist)
+        out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
+                      "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
+        if rank == 0 and not args.no_roofline:
+            out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps)
+        del plan
+        m.plans.clear()
+    if args.model in ("frcnn", "both"):
+        B = args.frcnn_batch
+        m = models.fasterrcnn_resnet50_fpn_v2().to("cuda")
+        plan = m.plan(B, 640, 640)
+        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 50).cuda())
+        plan.capture(stream)
+        el = timed_steps(plan, stream, max(1, args.steps // 2), max(1, args.warmup // 2), dist)
+        steps = max(1, args.steps // 2)
+        R = float(plan.proposal_count.tensor().float().mean().item())
+        gflop = 2 * (151.45e9 + 128.92e6 * R) / 1e9
+        out["frcnn"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
+                        "proposals_per_img": R, "dets_per_img": float(plan.out_count.tensor().float().mean().item()),
+                        "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2)}
+        if rank == 0 and not args.no_roofline:
+            out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps)
+        del plan
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    primary = "ssd" if "ssd" in out else "frcnn"
+    p = out[primary]
+    line = {
+        "metric": "images/sec/GPU at 640x640 (SSDLite & FRCNN-R50); ORIE max-abs-diff vs ref",
+        "value": round(p["value"], 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(p["ms_per_step"], 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "ssdlite320_mobilenet_v3_large b=%d 640x640 (configs[1])" % p["batch"]
+                   if primary == "ssd" else "fasterrcnn_resnet50_fpn_v2 b=%d 640x640 (configs[2])" % p["batch"],
+                   "global_batch": p["batch"] * world, "parallelism": f"dp{world}",
+                   "weights": "seeded synthetic (COCO weights need a download)"},
+    }
+    if "frcnn" in out and primary == "ssd":
+        f = out["frcnn"]
+        line["frcnn"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items() if k != "roofline"}
+        if "roofline" in f:
+            line["frcnn"]["roofline"] = f["roofline"]
+    if "roofline" in p:
+        line["roofline"] = p["roofline"]
+    line["dets_per_img"] = p.get("dets_per_img")
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(primary, args.cpu_budget)
+        if "frcnn" in out and primary == "ssd":
+            line["frcnn"]["cpu_baseline"] = cpu_baseline("frcnn", args.cpu_budget)
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,302 @@
+// Implicit-GEMM convolution on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the ATen conv2d + eval BatchNorm2d (+ activation) layers of the torchvision backbones
+// and heads reached from torch_models/detect.py:78.
+//
+// GEMM view: C[M=B*Ho*Wo][N=Cout] = A[M][K=KH*KW*Cin] * W[N][K]^T, NHWC activations, weights
+// packed K-contiguous ([Cout][KH][KW][Cin], K zero-padded to a multiple of 32).  BN is folded
+// into W/bias on the host.  The epilogue fuses bias, an optional residual (ResNet identity, FPN
+// top-down nearest-upsample add), the activation and a strided store (so SSD head outputs land
+// directly in the concatenated [B, anchors, classes] layout).  SqueezeExcitation's channel scale
+// is fused into the A-operand load of the projection conv.
+//
+// Tile: block = WM x WN waves, each wave TM x TN 32x32 MFMA tiles; BK = 32 per LDS stage,
+// double-buffered through registers (one barrier per K stage).  In an MFMA step lane-half h of a
+// wave contributes k = 16h + 8q + t (q, t loop indices), so both operands are read from LDS as
+// contiguous f32x4s (ds_read_b128) from K-contiguous rows padded to 36 floats (conflict-free
+// for the b128 lane groups).
+#include "kernels.hpp"
+
+namespace edgedet {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;  // padded LDS row (floats)
+
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
+    constexpr int NT = WM * WN * 64;
+    constexpr int BM = WM * TM * 32;
+    constexpr int BN = WN * TN * 32;
+    constexpr int AJ = BM * 8 / NT;  // f32x4 A loads per thread per stage
+    constexpr int BJ = BN * 8 / NT;
+    static_assert(AJ >= 1 && BJ >= 1, "tile too small for block");
+
+    __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
+    float* As = lds;
+    float* Bs = lds + 2 * BM * LDK;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wave_m = wid / WN;
+    const int wave_n = wid % WN;
+
+    // XCD-aware, bijective block remap: blocks that share an XCD (bid % 8) get consecutive tiles,
+    // which share their A (activation) panel.
+    const int nmt = (p.M + BM - 1) / BM;
+    const int nnt = (p.Cout + BN - 1) / BN;
+    const int nwg = nmt * nnt;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int mt = bid / nnt;
+    const int nt = bid % nnt;
+    const int m0 = mt * BM;
+    const int n0 = nt * BN;
+
+    // ---- per-thread A rows (fixed across K stages)
+    const int c4 = tid & 7;  // f32x4 column within the 32-wide stage
+    int64_t a_base[AJ];
+    int a_ih0[AJ], a_iw0[AJ], a_b[AJ];
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+        const int row = (tid >> 3) + (NT / 8) * j;
+        const int m = m0 + row;
+        if (m < p.M) {
+            const int b = (int)fdiv((uint32_t)m, p.div_howo);
+            const int rem = m - b * p.Ho * p.Wo;
+            const int oh = (int)fdiv((uint32_t)rem, p.div_wo);
+            const int ow = rem - oh * p.Wo;
+            a_b[j] = b;
+            a_base[j] = (int64_t)b * p.x_bstride;
+            a_ih0[j] = oh * p.stride - p.pad;
+            a_iw0[j] = ow * p.stride - p.pad;
+        } else {
+            a_b[j] = 0;
+            a_base[j] = 0;
+            a_ih0[j] = -(1 << 28);  // forces out-of-bounds -> zero
+            a_iw0[j] = 0;
+        }
+    }
+    const int KHW = p.KH * p.KW;
+
+    f32x4 ra[AJ], rb[BJ];
+
+    auto load_stage = [&](int k0) {
+        const int k = k0 + c4 * 4;
+        const int tap = (int)fdiv((uint32_t)k, p.div_cin);
+        const int ci = k - tap * p.Cin;
+        const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+        const int kw = tap - kh * p.KW;
+        const bool kval = tap < KHW;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
+                if (p.in_scale) {
+                    const f32x4 s = *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                    v.x *= s.x;
+                    v.y *= s.y;
+                    v.z *= s.z;
+                    v.w *= s.w;
+                }
+            }
+            ra[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int row = (tid >> 3) + (NT / 8) * j;
+            const int n = n0 + row;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (n < p.Cout) v = *reinterpret_cast<const f32x4*>(p.w + (int64_t)n * p.Kpad + k0 + c4 * 4);
+            rb[j] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        float* A = As + buf * BM * LDK;
+        float* Bb = Bs + buf * BN * LDK;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int row = (tid >> 3) + (NT / 8) * j;
+            *reinterpret_cast<f32x4*>(A + row * LDK + c4 * 4) = ra[j];
+        }
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int row = (tid >> 3) + (NT / 8) * j;
+            *reinterpret_cast<f32x4*>(Bb + row * LDK + c4 * 4) = rb[j];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = p.Kpad / BK;
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) load_stage((kc + 1) * BK);
+        const float* A = As + buf * BM * LDK;
+        const float* Bb = Bs + buf * BN * LDK;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            f32x4 af[TM][2], bf[TN][2];
+            const int kofs = 16 * h + 8 * q;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float* src = A + (wave_m * TM * 32 + i * 32 + l32) * LDK + kofs;
+                af[i][0] = *reinterpret_cast<const f32x4*>(src);
+                af[i][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const float* src = Bb + (wave_n * TN * 32 + j * 32 + l32) * LDK + kofs;
+                bf[j][0] = *reinterpret_cast<const f32x4*>(src);
+                bf[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const float a = (t < 4) ? af[i][0][t & 3] : af[i][1][t & 3];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float b = (t < 4) ? bf[j][0][t & 3] : bf[j][1][t & 3];
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (kc + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: bias + residual + activation, strided store
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int m = m0 + wave_m * TM * 32 + i * 32 + row;
+            if (m >= p.M) continue;
+            const int b = (int)fdiv((uint32_t)m, p.div_howo);
+            const int pix = m - b * p.Ho * p.Wo;
+            float* yrow = p.y + p.y_off + (int64_t)b * p.y_bstride + (int64_t)pix * p.y_pstride;
+            const float* rrow = nullptr;
+            if (p.res) {
+                int rpix = pix;
+                if (p.res_H != p.Ho || p.res_W != p.Wo) {
+                    const int oh = (int)fdiv((uint32_t)pix, p.div_wo);
+                    const int ow = pix - oh * p.Wo;
+                    int ry = (int)floorf((float)oh * p.res_sh);
+                    int rx = (int)floorf((float)ow * p.res_sw);
+                    ry = ry < p.res_H - 1 ? ry : p.res_H - 1;
+                    rx = rx < p.res_W - 1 ? rx : p.res_W - 1;
+                    rpix = ry * p.res_W + rx;
+                }
+                rrow = p.res + (int64_t)b * p.res_bstride + (int64_t)rpix * p.res_pstride;
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wave_n * TN * 32 + j * 32 + l32;
+                if (n >= p.Cout) continue;
+                float v = acc[i][j][r] + p.bias[n];
+                if (rrow) v += rrow[n];
+                yrow[n] = apply_act(v, p.act);
+            }
+        }
+    }
+}
+
+template <int WM, int WN, int TM, int TN>
+static int launch_cfg(const ConvParams& p, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, BN);
+    EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
+    hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, TM, TN>), dim3((unsigned)nwg), dim3(WM * WN * 64), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// Host launcher shared by the plan executor and the unit C entry point.
+int conv_launch(ConvParams p, int tile, hipStream_t s) {
+    EDGEDET_REQUIRE(p.Cin % 4 == 0, "conv: Cin must be a multiple of 4 (pad channels)");
+    EDGEDET_REQUIRE(p.x_pstride % 4 == 0, "conv: input pixel stride must be a multiple of 4");
+    EDGEDET_REQUIRE(p.Kpad % BK == 0 && p.Kpad >= p.K, "conv: Kpad must be a multiple of 32 and >= K");
+    EDGEDET_REQUIRE(p.M > 0 && p.Cout > 0, "conv: empty problem");
+    EDGEDET_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.w & 15) == 0, "conv: x/w must be 16-byte aligned");
+    EDGEDET_REQUIRE((int64_t)p.B * p.Ho * p.Wo < (1ll << 31), "conv: M overflows int32");
+    p.div_howo = make_fastdiv((uint32_t)(p.Ho * p.Wo));
+    p.div_wo = make_fastdiv((uint32_t)p.Wo);
+    p.div_cin = make_fastdiv((uint32_t)p.Cin);
+    p.div_kw = make_fastdiv((uint32_t)p.KW);
+    if (p.res_H <= 0) p.res_H = p.Ho;
+    if (p.res_W <= 0) p.res_W = p.Wo;
+    p.res_sh = (float)p.res_H / (float)p.Ho;
+    p.res_sw = (float)p.res_W / (float)p.Wo;
+    if (tile <= 0) tile = p.Cout <= 32 ? 1 : (p.Cout <= 64 ? 2 : 3);
+    switch (tile) {
+        case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
+        case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
+        case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128
+        case 4: return launch_cfg<4, 2, 2, 2>(p, s);  // 256 x 128
+        default: EDGEDET_REQUIRE(false, "conv: unknown tile config");
+    }
+}
+
+}  // namespace edgedet
+
+using namespace edgedet;
+
+extern "C" int64_t edgedet_conv_weight_k(int32_t KH, int32_t KW, int64_t Cin) {
+    return cdiv((int64_t)KH * KW * Cin, BK) * BK;
+}
+
+extern "C" int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                              const float* bias, int64_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                              int32_t pad, int32_t act, const float* res, float* y, void* stream) {
+    ConvParams p{};
+    p.x = x;
+    p.w = w;
+    p.bias = bias;
+    p.y = y;
+    p.res = res;
+    p.B = (int)B;
+    p.H = (int)H;
+    p.W = (int)W;
+    p.Cin = (int)Cin;
+    p.Cout = (int)Cout;
+    p.KH = KH;
+    p.KW = KW;
+    p.stride = stride;
+    p.pad = pad;
+    p.act = act;
+    p.Ho = (int)((H + 2 * pad - KH) / stride + 1);
+    p.Wo = (int)((W + 2 * pad - KW) / stride + 1);
+    p.K = (int)(KH * KW * Cin);
+    p.Kpad = (int)edgedet_conv_weight_k(KH, KW, Cin);
+    p.M = (int)(B * p.Ho * p.Wo);
+    p.x_pstride = (int)Cin;
+    p.x_bstride = H * W * Cin;
+    p.y_pstride = (int)Cout;
+    p.y_bstride = (int64_t)p.Ho * p.Wo * Cout;
+    p.res_pstride = (int)Cout;
+    p.res_bstride = p.y_bstride;
+    return conv_launch(p, 0, (hipStream_t)stream);
+}

@@ -1,0 +1,309 @@
+// Native plan executor of libedgedet.so.
+//
+// A detector forward is lowered by the Python host (edgeml_amd/plan.py) into a flat array of
+// edgedet_op records; this file decodes each record into its kernel's parameter block and launches
+// it on the caller's stream, or captures the whole sequence once into a hipGraph that is replayed
+// per batch (one host call per forward; no allocation, no sync, no host round trip inside).
+//
+// Record layouts (i = int64 fields, p = device pointers, d = doubles, f = floats):
+//   MEMSET         p0 ptr; i0 bytes
+//   PREPROCESS     p0 x[B,3,H,W]; p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
+//   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0;
+//                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
+//                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
+//                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
+//   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act
+//   CHANNEL_MEAN   p0 x[B,HW,C]; p1 out[B,C]; i0..2 B,HW,C
+//   SE_FC          p0 mean; p1 w1t[C][S]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; i0..2 B,C,S
+//   MAXPOOL        p0 x; p1 y; i0..8 B,H,W,C,Ho,Wo,K,stride,pad
+//   SSD_SCORES     p0 logits[B,A,NC]; p1 reg[B,A,4]; p2 anchors[A,4]; p3 scores_t[B,NC,A];
+//                  p4 boxes[B,A,4]; i0..2 B,A,NC; f0,f1 img_h,img_w
+//   SSD_CLASS_NMS  p0 scores_t; p1 boxes; p2..6 records (box,score,tb,label,count);
+//                  i0..4 B,A,NC,topk,kmax; f0 score_thresh; d0 iou
+//   MERGE_TOPK     p0..4 records; p5 ratio[B,2]|0; p6 out_box; p7 out_score; p8 out_label|0;
+//                  p9 out_count; i0..3 B,S,kmax,N
+//   RPN_LEVEL_NMS  p0..4 head per level; p5..9 anchors per level; p10..14 records;
+//                  i0..5 B,nlevels,ld,A,topk,kmax; i6..10 n per level;
+//                  f0..3 img_h,img_w,min_size,score_thresh; d0 iou
+//   ROI_ALIGN      p0..3 feats; p4 rois; p5 counts; p6 out; i0..10 mode,R,RMAX,B,C,PH,PW,sr,nlevels,
+//                  k_min,k_max; i11..14 H; i15..18 W; f0..3 scales
+//   BOX_SCORES     p0 pred; p1 props; p2 counts; p3 scores; p4 boxes; i0..5 ld,B,R,NC,cls_off,delta_off;
+//                  f0,f1 img_h,img_w
+//   BOX_CLASS_NMS  p0 scores; p1 boxes; p2 counts; p3..7 records; i0..3 B,R,NC,kmax;
+//                  f0 score_thresh; f1 min_size; d0 iou
+#include <mutex>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace edgedet {
+
+static thread_local std::string g_error;
+void set_error(const std::string& msg) { g_error = msg; }
+const char* get_error() { return g_error.c_str(); }
+
+template <typename T>
+static T* P(const edgedet_op& o, int k) {
+    return reinterpret_cast<T*>(static_cast<uintptr_t>(o.p[k]));
+}
+
+static SegOut seg_out(const edgedet_op& o, int k0, int kmax) {
+    SegOut s;
+    s.box = P<f32x4>(o, k0);
+    s.score = P<float>(o, k0 + 1);
+    s.tb = P<uint32_t>(o, k0 + 2);
+    s.label = P<int>(o, k0 + 3);
+    s.count = P<int>(o, k0 + 4);
+    s.kmax = kmax;
+    return s;
+}
+
+static int run_op(const edgedet_op& o, hipStream_t s) {
+    const int64_t* I = o.i;
+    switch (o.kind) {
+        case EDGEDET_OP_MEMSET:
+            EDGEDET_CHECK_HIP(hipMemsetAsync(P<void>(o, 0), 0, (size_t)I[0], s));
+            return 0;
+        case EDGEDET_OP_PREPROCESS: {
+            PreParams p{};
+            p.x = P<const float>(o, 0);
+            p.y = P<float>(o, 1);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.Ho = (int)I[3];
+            p.Wo = (int)I[4];
+            p.Hp = (int)I[5];
+            p.Wp = (int)I[6];
+            for (int c = 0; c < 3; ++c) {
+                p.mean[c] = o.f[c];
+                p.stdv[c] = o.f[3 + c];
+            }
+            return preprocess_launch(p, s);
+        }
+        case EDGEDET_OP_CONV: {
+            ConvParams p{};
+            p.x = P<const float>(o, 0);
+            p.w = P<const float>(o, 1);
+            p.bias = P<const float>(o, 2);
+            p.y = P<float>(o, 3);
+            p.res = P<const float>(o, 4);
+            p.in_scale = P<const float>(o, 5);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.Cin = (int)I[3];
+            p.Ho = (int)I[4];
+            p.Wo = (int)I[5];
+            p.Cout = (int)I[6];
+            p.KH = (int)I[7];
+            p.KW = (int)I[8];
+            p.stride = (int)I[9];
+            p.pad = (int)I[10];
+            p.act = (int)I[11];
+            p.K = (int)I[12];
+            p.Kpad = (int)I[13];
+            p.x_pstride = (int)I[14];
+            p.y_pstride = (int)I[15];
+            p.res_pstride = (int)I[16];
+            p.x_bstride = I[17];
+            p.y_bstride = I[18];
+            p.res_bstride = I[19];
+            p.y_off = I[20];
+            p.res_H = (int)I[21];
+            p.res_W = (int)I[22];
+            p.M = p.B * p.Ho * p.Wo;
+            EDGEDET_REQUIRE(p.K == p.KH * p.KW * p.Cin, "conv: K != KH*KW*Cin");
+            return conv_launch(p, (int)I[23], s);
+        }
+        case EDGEDET_OP_DWCONV: {
+            DwParams p{};
+            p.x = P<const float>(o, 0);
+            p.w = P<const float>(o, 1);
+            p.bias = P<const float>(o, 2);
+            p.y = P<float>(o, 3);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.C = (int)I[3];
+            p.Ho = (int)I[4];
+            p.Wo = (int)I[5];
+            p.K = (int)I[6];
+            p.stride = (int)I[7];
+            p.pad = (int)I[8];
+            p.act = (int)I[9];
+            return dwconv_launch(p, s);
+        }
+        case EDGEDET_OP_CHANNEL_MEAN:
+            return channel_mean_launch(P<const float>(o, 0), P<float>(o, 1), (int)I[0], (int)I[1], (int)I[2], s);
+        case EDGEDET_OP_SE_FC:
+            return se_fc_launch(P<const float>(o, 0), P<const float>(o, 1), P<const float>(o, 2), P<const float>(o, 3),
+                                P<const float>(o, 4), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2], s);
+        case EDGEDET_OP_MAXPOOL: {
+            PoolParams p{};
+            p.x = P<const float>(o, 0);
+            p.y = P<float>(o, 1);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.C = (int)I[3];
+            p.Ho = (int)I[4];
+            p.Wo = (int)I[5];
+            p.K = (int)I[6];
+            p.stride = (int)I[7];
+            p.pad = (int)I[8];
+            return maxpool_launch(p, s);
+        }
+        case EDGEDET_OP_SSD_SCORES:
+            return ssd_scores_launch(P<const float>(o, 0), P<const float>(o, 1), P<const float>(o, 2), P<float>(o, 3),
+                                     P<float>(o, 4), (int)I[0], (int)I[1], (int)I[2], o.f[0], o.f[1], s);
+        case EDGEDET_OP_SSD_CLASS_NMS:
+            return ssd_class_nms_launch(P<const float>(o, 0), P<const float>(o, 1), (int)I[0], (int)I[1], (int)I[2],
+                                        o.f[0], (int)I[3], o.d[0], seg_out(o, 2, (int)I[4]), s);
+        case EDGEDET_OP_MERGE_TOPK: {
+            MergeParams p{};
+            p.box = P<const f32x4>(o, 0);
+            p.score = P<const float>(o, 1);
+            p.tb = P<const uint32_t>(o, 2);
+            p.label = P<const int>(o, 3);
+            p.count = P<const int>(o, 4);
+            p.ratio = P<const float>(o, 5);
+            p.out_box = P<float>(o, 6);
+            p.out_score = P<float>(o, 7);
+            p.out_label = P<int64_t>(o, 8);
+            p.out_count = P<int>(o, 9);
+            p.S = (int)I[1];
+            p.kmax = (int)I[2];
+            p.N = (int)I[3];
+            return merge_topk_launch(p, (int)I[0], s);
+        }
+        case EDGEDET_OP_RPN_LEVEL_NMS: {
+            RpnParams p{};
+            p.B = (int)I[0];
+            p.nlevels = (int)I[1];
+            p.ld = (int)I[2];
+            p.A = (int)I[3];
+            p.topk = (int)I[4];
+            EDGEDET_REQUIRE(p.nlevels >= 1 && p.nlevels <= 5, "rpn: 1..5 levels");
+            for (int l = 0; l < p.nlevels; ++l) {
+                p.lv[l].head = P<const float>(o, l);
+                p.lv[l].anchors = P<const float>(o, 5 + l);
+                p.lv[l].n = (int)I[6 + l];
+            }
+            p.img_h = o.f[0];
+            p.img_w = o.f[1];
+            p.min_size = o.f[2];
+            p.score_thresh = o.f[3];
+            p.iou = o.d[0];
+            return rpn_level_nms_launch(p, seg_out(o, 10, (int)I[5]), s);
+        }
+        case EDGEDET_OP_ROI_ALIGN: {
+            RoiParams p{};
+            for (int l = 0; l < 4; ++l) {
+                p.feat[l] = P<const float>(o, l);
+                p.H[l] = (int)I[11 + l];
+                p.W[l] = (int)I[15 + l];
+                p.scale[l] = o.f[l];
+            }
+            p.rois = P<const float>(o, 4);
+            p.counts = P<const int>(o, 5);
+            p.out = P<float>(o, 6);
+            p.mode = (int)I[0];
+            p.R = (int)I[1];
+            p.RMAX = (int)I[2];
+            p.B = (int)I[3];
+            p.C = (int)I[4];
+            p.PH = (int)I[5];
+            p.PW = (int)I[6];
+            p.sr = (int)I[7];
+            p.nlevels = (int)I[8];
+            p.k_min = (int)I[9];
+            p.k_max = (int)I[10];
+            return roi_align_launch(p, s);
+        }
+        case EDGEDET_OP_BOX_SCORES:
+            return box_scores_launch(P<const float>(o, 0), (int)I[0], (int)I[4], (int)I[5], P<const float>(o, 1),
+                                     P<const int>(o, 2), P<float>(o, 3), P<float>(o, 4), (int)I[1], (int)I[2],
+                                     (int)I[3], o.f[0], o.f[1], s);
+        case EDGEDET_OP_BOX_CLASS_NMS:
+            return box_class_nms_launch(P<const float>(o, 0), P<const float>(o, 1), P<const int>(o, 2), (int)I[0],
+                                        (int)I[1], (int)I[2], o.f[0], o.f[1], o.d[0], seg_out(o, 3, (int)I[3]), s);
+        default:
+            set_error("edgedet: unknown op kind " + std::to_string(o.kind));
+            return -1;
+    }
+}
+
+static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
+    for (int64_t k = 0; k < n; ++k) {
+        const int rc = run_op(ops[k], s);
+        if (rc != 0) {
+            set_error("op " + std::to_string(k) + " (kind " + std::to_string(ops[k].kind) + "): " + g_error);
+            return rc;
+        }
+    }
+    return 0;
+}
+
+struct Graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+}  // namespace edgedet
+
+using namespace edgedet;
+
+extern "C" int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream) {
+    return run_ops(ops, n, (hipStream_t)stream);
+}
+
+extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** out) {
+    hipStream_t s = (hipStream_t)stream;
+    EDGEDET_REQUIRE(s != nullptr, "graph capture needs a non-default stream");
+    Graph* g = new Graph();
+    EDGEDET_CHECK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int rc = run_ops(ops, n, s);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &graph);
+    if (rc != 0) {
+        if (graph) (void)hipGraphDestroy(graph);
+        delete g;
+        return rc;
+    }
+    if (e != hipSuccess) {
+        delete g;
+        set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        return -2;
+    }
+    g->graph = graph;
+    const hipError_t e2 = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+    if (e2 != hipSuccess) {
+        (void)hipGraphDestroy(graph);
+        delete g;
+        set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e2));
+        return -2;
+    }
+    *out = g;
+    return 0;
+}
+
+extern "C" int edgedet_graph_launch(void* graph, void* stream) {
+    Graph* g = reinterpret_cast<Graph*>(graph);
+    EDGEDET_REQUIRE(g && g->exec, "graph_launch: null graph");
+    EDGEDET_CHECK_HIP(hipGraphLaunch(g->exec, (hipStream_t)stream));
+    return 0;
+}
+
+extern "C" int edgedet_graph_destroy(void* graph) {
+    Graph* g = reinterpret_cast<Graph*>(graph);
+    if (!g) return 0;
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    delete g;
+    return 0;
+}
+
+extern "C" const char* edgedet_last_error(void) { return get_error(); }
+extern "C" int32_t edgedet_version(void) { return (1 << 16) | 0; }
+extern "C" const char* edgedet_target(void) { return "gfx950"; }

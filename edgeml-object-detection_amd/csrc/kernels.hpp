@@ -1,0 +1,113 @@
+// Parameter blocks and host launchers of every kernel (shared by the .hip units and exec.hip).
+#pragma once
+#include "common.hpp"
+
+namespace edgedet {
+
+struct ConvParams {
+    const float* x;
+    const float* w;
+    const float* bias;
+    float* y;
+    const float* res;
+    const float* in_scale;  // [B][Cin] or null (SE excitation)
+    int B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, act;
+    int K, Kpad, M;
+    int x_pstride, y_pstride, res_pstride;
+    int64_t x_bstride, y_bstride, res_bstride, y_off;
+    int res_H, res_W;
+    float res_sh, res_sw;  // nearest-upsample scales (in/out) for the residual
+    FastDiv div_howo, div_wo, div_cin, div_kw;
+};
+
+struct PreParams {
+    const float* x;  // [B][3][H][W]
+    float* y;        // [B][Hp][Wp][4]
+    int B, H, W, Ho, Wo, Hp, Wp;
+    float mean[3], stdv[3];
+    float sh, sw;  // input/output scales
+};
+
+struct DwParams {
+    const float* x;  // [B][H][W][C]
+    const float* w;  // [K*K][C]
+    const float* bias;
+    float* y;        // [B][Ho][Wo][C]
+    int B, H, W, C, Ho, Wo, K, stride, pad, act;
+};
+
+struct PoolParams {
+    const float* x;
+    float* y;
+    int B, H, W, C, Ho, Wo, K, stride, pad;
+};
+
+struct RoiParams {
+    const float* feat[4];  // NHWC per level
+    int H[4], W[4];
+    float scale[4];
+    int nlevels;
+    const float* rois;      // mode 0: [R][5] (b, x1, y1, x2, y2); mode 1: boxes [B][RMAX][4]
+    const int* counts;      // mode 1: valid rois per image
+    int mode, R, RMAX, B, C, PH, PW, sr;
+    int k_min, k_max;       // LevelMapper levels (mode 1)
+    float* out;             // [R][PH][PW][C]
+};
+
+struct SegOut {
+    f32x4* box;     // [B*S][kmax]
+    float* score;   // [B*S][kmax]
+    uint32_t* tb;   // [B*S][kmax] merge tiebreak (position of the candidate in the reference's
+                    //              concatenated candidate list, order-preserving)
+    int* label;     // [B*S][kmax]
+    int* count;     // [B*S]
+    int kmax;
+};
+
+struct RpnLevel {
+    const float* head;     // [B][HW][ld]: objectness at [a], deltas at [A + 4a + 0..3]
+    const float* anchors;  // [HW*A][4]
+    int n;                 // HW*A
+};
+
+struct RpnParams {
+    RpnLevel lv[5];
+    int nlevels, ld, A, B, topk;
+    float img_h, img_w, min_size, score_thresh;
+    double iou;
+};
+
+struct MergeParams {
+    const f32x4* box;
+    const float* score;
+    const uint32_t* tb;
+    const int* label;
+    const int* count;    // [B][S]
+    int S, kmax, N;
+    const float* ratio;  // [B][2] (rw, rh) or null
+    float* out_box;      // [B][N][4]
+    float* out_score;    // [B][N]
+    int64_t* out_label;  // [B][N] or null
+    int* out_count;      // [B]
+};
+
+int conv_launch(ConvParams p, int tile, hipStream_t s);
+int preprocess_launch(const PreParams& p, hipStream_t s);
+int dwconv_launch(const DwParams& p, hipStream_t s);
+int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);
+int se_fc_launch(const float* mean, const float* w1t, const float* b1, const float* w2t, const float* b2,
+                 float* scale, int B, int C, int S, hipStream_t s);
+int maxpool_launch(const PoolParams& p, hipStream_t s);
+int roi_align_launch(const RoiParams& p, hipStream_t s);
+int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,
+                      int B, int A, int NC, float img_h, float img_w, hipStream_t s);
+int box_scores_launch(const float* pred, int ld, int cls_off, int delta_off, const float* props, const int* counts,
+                      float* scores, float* boxes, int B, int R, int NC, float img_h, float img_w, hipStream_t s);
+int ssd_class_nms_launch(const float* scores_t, const float* boxes, int B, int A, int NC, float score_thresh,
+                         int topk, double iou, SegOut out, hipStream_t s);
+int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s);
+int box_class_nms_launch(const float* scores, const float* boxes, const int* counts, int B, int R, int NC,
+                         float score_thresh, float min_size, double iou, SegOut out, hipStream_t s);
+int merge_topk_launch(const MergeParams& P, int B, hipStream_t s);
+
+}  // namespace edgedet

@@ -1,0 +1,371 @@
+// Memory-bound layers of the two detectors (NHWC fp32, one thread per pixel x 4 channels).
+//
+//   preprocess   GeneralizedRCNNTransform eval: (x - mean) / std, bilinear resize
+//                (align_corners=False), zero pad to the batch size        SURVEY.md App. A.0, row a6
+//   dwconv       depthwise conv + folded BN + act (MobileNetV3 / SSDLite)  App. A.1, rows a7/a8
+//   channel_mean adaptive_avg_pool2d(1) of SqueezeExcitation               App. A.1 step 2
+//   se_fc        SE fc1 -> ReLU -> fc2 -> Hardsigmoid (per image)          App. A.1 step 2
+//   maxpool      ResNet stem max_pool2d(3,2,1); FPN LastLevelMaxPool(1,2,0) App. A.2 steps 2-3
+//   roi_align    MultiScaleRoIAlign: LevelMapper + roi_align(7x7, sr=2, aligned=False)
+//                                                                          App. A.2 step 5, row a13
+#include "kernels.hpp"
+
+namespace edgedet {
+
+
+// ------------------------------------------------------------------------------ preprocess
+
+__global__ void preprocess_kernel(PreParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
+    if (idx >= total) return;
+    const int ox = (int)(idx % p.Wp);
+    const int oy = (int)((idx / p.Wp) % p.Hp);
+    const int b = (int)(idx / ((int64_t)p.Wp * p.Hp));
+    f32x4 out = {0.f, 0.f, 0.f, 0.f};
+    if (oy < p.Ho && ox < p.Wo) {
+        // ATen area_pixel_compute_source_index (align_corners=False, linear)
+        float ry = p.sh * ((float)oy + 0.5f) - 0.5f;
+        float rx = p.sw * ((float)ox + 0.5f) - 0.5f;
+        ry = ry < 0.f ? 0.f : ry;
+        rx = rx < 0.f ? 0.f : rx;
+        const int y0 = (int)ry, x0 = (int)rx;
+        const int y1 = y0 + ((y0 < p.H - 1) ? 1 : 0);
+        const int x1 = x0 + ((x0 < p.W - 1) ? 1 : 0);
+        const float ly = ry - (float)y0, lx = rx - (float)x0;
+        const float hy = 1.f - ly, hx = 1.f - lx;
+        float v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float* src = p.x + ((int64_t)b * 3 + c) * p.H * p.W;
+            const float a00 = (src[(int64_t)y0 * p.W + x0] - p.mean[c]) / p.stdv[c];
+            const float a01 = (src[(int64_t)y0 * p.W + x1] - p.mean[c]) / p.stdv[c];
+            const float a10 = (src[(int64_t)y1 * p.W + x0] - p.mean[c]) / p.stdv[c];
+            const float a11 = (src[(int64_t)y1 * p.W + x1] - p.mean[c]) / p.stdv[c];
+            v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
+        }
+        out = f32x4{v[0], v[1], v[2], 0.f};
+    }
+    *reinterpret_cast<f32x4*>(p.y + idx * 4) = out;
+}
+
+int preprocess_launch(const PreParams& p0, hipStream_t s) {
+    PreParams p = p0;
+    EDGEDET_REQUIRE(p.Hp >= p.Ho && p.Wp >= p.Wo && p.Ho > 0 && p.Wo > 0, "preprocess: bad sizes");
+    p.sh = (float)p.H / (float)p.Ho;
+    p.sw = (float)p.W / (float)p.Wo;
+    const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
+    hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ depthwise
+
+__global__ void dwconv_kernel(DwParams p) {
+    const int C4 = p.C >> 2;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.B * p.Ho * p.Wo * C4;
+    if (idx >= total) return;
+    const int c = (int)(idx % C4) * 4;
+    const int64_t pix = idx / C4;
+    const int ow = (int)(pix % p.Wo);
+    const int oh = (int)((pix / p.Wo) % p.Ho);
+    const int b = (int)(pix / ((int64_t)p.Wo * p.Ho));
+    const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
+    for (int kh = 0; kh < p.K; ++kh) {
+        const int ih = ih0 + kh;
+        if ((unsigned)ih >= (unsigned)p.H) continue;
+        for (int kw = 0; kw < p.K; ++kw) {
+            const int iw = iw0 + kw;
+            if ((unsigned)iw >= (unsigned)p.W) continue;
+            const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * p.C);
+            const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * p.K + kw) * p.C + c);
+            acc.x = fmaf(xv.x, wv.x, acc.x);
+            acc.y = fmaf(xv.y, wv.y, acc.y);
+            acc.z = fmaf(xv.z, wv.z, acc.z);
+            acc.w = fmaf(xv.w, wv.w, acc.w);
+        }
+    }
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+    f32x4 o;
+    o.x = apply_act(acc.x + bv.x, p.act);
+    o.y = apply_act(acc.y + bv.y, p.act);
+    o.z = apply_act(acc.z + bv.z, p.act);
+    o.w = apply_act(acc.w + bv.w, p.act);
+    *reinterpret_cast<f32x4*>(p.y + pix * p.C + c) = o;
+}
+
+int dwconv_launch(const DwParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
+    const int64_t total = (int64_t)p.B * p.Ho * p.Wo * (p.C / 4);
+    hipLaunchKernelGGL(dwconv_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ SE squeeze
+// grid (cdiv(C, 64), B), block 256 = 64 channels x 4 pixel groups.
+__global__ void channel_mean_kernel(const float* __restrict__ x, float* __restrict__ out, int HW, int C) {
+    __shared__ float part[4][64];
+    const int b = blockIdx.y;
+    const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    float s = 0.f;
+    if (c < C) {
+        const float* xb = x + (int64_t)b * HW * C + c;
+        for (int i = g; i < HW; i += 4) s += xb[(int64_t)i * C];
+    }
+    part[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < C) out[(int64_t)b * C + c] = (((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl]) / (float)HW;
+}
+
+int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s) {
+    hipLaunchKernelGGL(channel_mean_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), 0, s, x, out, HW, C);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ SE excitation
+// One block per image.  w1t [C][S] (fc1 transposed), w2t [S][C] (fc2 transposed).
+__global__ void se_fc_kernel(const float* __restrict__ mean, const float* __restrict__ w1t,
+                             const float* __restrict__ b1, const float* __restrict__ w2t,
+                             const float* __restrict__ b2, float* __restrict__ scale, int C, int S) {
+    extern __shared__ float sm[];
+    float* m = sm;      // [C]
+    float* s1 = sm + C; // [S]
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) m[c] = mean[(int64_t)b * C + c];
+    __syncthreads();
+    for (int j = threadIdx.x; j < S; j += blockDim.x) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a = fmaf(w1t[(int64_t)c * S + j], m[c], a);
+        a += b1[j];
+        s1[j] = a > 0.f ? a : 0.f;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float a = 0.f;
+        for (int j = 0; j < S; ++j) a = fmaf(w2t[(int64_t)j * C + c], s1[j], a);
+        scale[(int64_t)b * C + c] = apply_act(a + b2[c], ACT_HSIGMOID);
+    }
+}
+
+int se_fc_launch(const float* mean, const float* w1t, const float* b1, const float* w2t, const float* b2,
+                 float* scale, int B, int C, int S, hipStream_t s) {
+    const size_t lds = (size_t)(C + S) * sizeof(float);
+    EDGEDET_REQUIRE(lds <= 60 * 1024, "se_fc: too many channels");
+    hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), lds, s, mean, w1t, b1, w2t, b2, scale, C, S);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ max pool
+
+__global__ void maxpool_kernel(PoolParams p) {
+    const int C4 = p.C >> 2;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.B * p.Ho * p.Wo * C4;
+    if (idx >= total) return;
+    const int c = (int)(idx % C4) * 4;
+    const int64_t pix = idx / C4;
+    const int ow = (int)(pix % p.Wo);
+    const int oh = (int)((pix / p.Wo) % p.Ho);
+    const int b = (int)(pix / ((int64_t)p.Wo * p.Ho));
+    const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
+    const float ninf = -__builtin_inff();
+    f32x4 m = {ninf, ninf, ninf, ninf};
+    for (int kh = 0; kh < p.K; ++kh) {
+        const int ih = oh * p.stride - p.pad + kh;
+        if ((unsigned)ih >= (unsigned)p.H) continue;
+        for (int kw = 0; kw < p.K; ++kw) {
+            const int iw = ow * p.stride - p.pad + kw;
+            if ((unsigned)iw >= (unsigned)p.W) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * p.C);
+            // ATen max_pool2d: NaN propagates, otherwise max
+            m.x = (v.x > m.x || isnan(v.x)) ? v.x : m.x;
+            m.y = (v.y > m.y || isnan(v.y)) ? v.y : m.y;
+            m.z = (v.z > m.z || isnan(v.z)) ? v.z : m.z;
+            m.w = (v.w > m.w || isnan(v.w)) ? v.w : m.w;
+        }
+    }
+    *reinterpret_cast<f32x4*>(p.y + pix * p.C + c) = m;
+}
+
+int maxpool_launch(const PoolParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.C % 4 == 0, "maxpool: C must be a multiple of 4");
+    const int64_t total = (int64_t)p.B * p.Ho * p.Wo * (p.C / 4);
+    hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ RoIAlign
+// torchvision roi_align (aligned=False) bilinear_interpolate, restated for NHWC features.
+__device__ __forceinline__ void bilinear_setup(float y, float x, int H, int W, int& o1, int& o2, int& o3, int& o4,
+                                               float& w1, float& w2, float& w3, float& w4) {
+    if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) {
+        o1 = o2 = o3 = o4 = 0;
+        w1 = w2 = w3 = w4 = 0.f;
+        return;
+    }
+    if (y <= 0.f) y = 0.f;
+    if (x <= 0.f) x = 0.f;
+    int y_low = (int)y, x_low = (int)x, y_high, x_high;
+    if (y_low >= H - 1) {
+        y_high = y_low = H - 1;
+        y = (float)y_low;
+    } else {
+        y_high = y_low + 1;
+    }
+    if (x_low >= W - 1) {
+        x_high = x_low = W - 1;
+        x = (float)x_low;
+    } else {
+        x_high = x_low + 1;
+    }
+    const float ly = y - (float)y_low, lx = x - (float)x_low;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    o1 = y_low * W + x_low;
+    o2 = y_low * W + x_high;
+    o3 = y_high * W + x_low;
+    o4 = y_high * W + x_high;
+    w1 = hy * hx;
+    w2 = hy * lx;
+    w3 = ly * hx;
+    w4 = ly * lx;
+}
+
+
+__global__ void roi_align_kernel(RoiParams p) {
+    const int C4 = p.C >> 2;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.R * p.PH * p.PW * C4;
+    if (idx >= total) return;
+    const int c = (int)(idx % C4) * 4;
+    int64_t t = idx / C4;
+    const int pw = (int)(t % p.PW);
+    t /= p.PW;
+    const int ph = (int)(t % p.PH);
+    const int r = (int)(t / p.PH);
+    float* o = p.out + idx * 4;
+    int b, lvl = 0;
+    float x1, y1, x2, y2;
+    if (p.mode == 0) {
+        const float* rr = p.rois + (int64_t)r * 5;
+        b = (int)rr[0];
+        x1 = rr[1];
+        y1 = rr[2];
+        x2 = rr[3];
+        y2 = rr[4];
+    } else {
+        b = r / p.RMAX;
+        const int slot = r - b * p.RMAX;
+        if (slot >= p.counts[b]) {
+            *reinterpret_cast<f32x4*>(o) = f32x4{0.f, 0.f, 0.f, 0.f};
+            return;
+        }
+        const float* bb = p.rois + (int64_t)r * 4;
+        x1 = bb[0];
+        y1 = bb[1];
+        x2 = bb[2];
+        y2 = bb[3];
+        // LevelMapper (canonical scale 224, level 4, eps 1e-6)
+        const float area = (x2 - x1) * (y2 - y1);
+        const float s = sqrtf(area);
+        float tl = floorf((4.0f + log2f(s / 224.0f)) + 1e-6f);
+        tl = fminf(fmaxf(tl, (float)p.k_min), (float)p.k_max);
+        lvl = (int)tl - p.k_min;
+    }
+    const float* f = p.feat[lvl];
+    const int H = p.H[lvl], W = p.W[lvl];
+    const float scale = p.scale[lvl];
+    const float rsw = x1 * scale, rsh = y1 * scale;
+    const float rew = x2 * scale, reh = y2 * scale;
+    float rw = rew - rsw, rh = reh - rsh;
+    rw = rw > 1.f ? rw : 1.f;
+    rh = rh > 1.f ? rh : 1.f;
+    const float bin_h = rh / (float)p.PH, bin_w = rw / (float)p.PW;
+    const int gh = p.sr > 0 ? p.sr : (int)ceilf(rh / (float)p.PH);
+    const int gw = p.sr > 0 ? p.sr : (int)ceilf(rw / (float)p.PW);
+    const int cnt = gh * gw;
+    const float count = (float)(cnt > 1 ? cnt : 1);
+    const float* fb = f + (int64_t)b * H * W * p.C + c;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int iy = 0; iy < gh; ++iy) {
+        const float yy = (rsh + (float)ph * bin_h) + ((float)iy + .5f) * bin_h / (float)gh;
+        for (int ix = 0; ix < gw; ++ix) {
+            const float xx = (rsw + (float)pw * bin_w) + ((float)ix + .5f) * bin_w / (float)gw;
+            int o1, o2, o3, o4;
+            float w1, w2, w3, w4;
+            bilinear_setup(yy, xx, H, W, o1, o2, o3, o4, w1, w2, w3, w4);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(fb + (int64_t)o1 * p.C);
+            const f32x4 v2 = *reinterpret_cast<const f32x4*>(fb + (int64_t)o2 * p.C);
+            const f32x4 v3 = *reinterpret_cast<const f32x4*>(fb + (int64_t)o3 * p.C);
+            const f32x4 v4 = *reinterpret_cast<const f32x4*>(fb + (int64_t)o4 * p.C);
+            acc.x += ((w1 * v1.x + w2 * v2.x) + w3 * v3.x) + w4 * v4.x;
+            acc.y += ((w1 * v1.y + w2 * v2.y) + w3 * v3.y) + w4 * v4.y;
+            acc.z += ((w1 * v1.z + w2 * v2.z) + w3 * v3.z) + w4 * v4.z;
+            acc.w += ((w1 * v1.w + w2 * v2.w) + w3 * v3.w) + w4 * v4.w;
+        }
+    }
+    *reinterpret_cast<f32x4*>(o) = f32x4{acc.x / count, acc.y / count, acc.z / count, acc.w / count};
+}
+
+int roi_align_launch(const RoiParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.C % 4 == 0, "roi_align: C must be a multiple of 4");
+    EDGEDET_REQUIRE(p.nlevels >= 1 && p.nlevels <= 4, "roi_align: 1..4 levels");
+    const int64_t total = (int64_t)p.R * p.PH * p.PW * (p.C / 4);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(roi_align_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace edgedet
+
+using namespace edgedet;
+
+extern "C" int edgedet_roi_align(const float* feat, int64_t B, int64_t H, int64_t W, int64_t C, const float* rois,
+                                 int64_t R, float spatial_scale, int32_t pooled_h, int32_t pooled_w,
+                                 int32_t sampling_ratio, float* out, void* stream) {
+    RoiParams p{};
+    p.feat[0] = feat;
+    p.H[0] = (int)H;
+    p.W[0] = (int)W;
+    p.scale[0] = spatial_scale;
+    p.nlevels = 1;
+    p.rois = rois;
+    p.mode = 0;
+    p.R = (int)R;
+    p.B = (int)B;
+    p.C = (int)C;
+    p.PH = pooled_h;
+    p.PW = pooled_w;
+    p.sr = sampling_ratio;
+    return roi_align_launch(p, (hipStream_t)stream);
+}
+
+extern "C" int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,
+                                const float* bias, int32_t K, int32_t stride, int32_t pad, int32_t act, float* y,
+                                void* stream) {
+    DwParams p{};
+    p.x = x;
+    p.w = w;
+    p.bias = bias;
+    p.y = y;
+    p.B = (int)B;
+    p.H = (int)H;
+    p.W = (int)W;
+    p.C = (int)C;
+    p.K = K;
+    p.stride = stride;
+    p.pad = pad;
+    p.act = act;
+    p.Ho = (int)((H + 2 * pad - K) / stride + 1);
+    p.Wo = (int)((W + 2 * pad - K) / stride + 1);
+    return dwconv_launch(p, (hipStream_t)stream);
+}

@@ -1,0 +1,135 @@
+"""Drop-in for torch_models/detect.py: same CLI, same output files, MI355X engine underneath.
+
+    python -m edgeml_amd.detect img_dir save_dir [--dataset coco|voc] [--model ssd|faster_rcnn]
+                                [--model-path PATH]
+
+Behaviour kept from the reference (detect.py:62-106): images are taken in sorted(os.listdir) order,
+read as RGB and scaled by 1/255, every image gets one ``<name[:-4]>.npy`` (N,6) float64 file
+``[cls, xc, yc, w, h, conf]`` normalised by the original size, rows in score order, an empty result
+still writes a (0,6) file.  Differences: images of equal size are batched (results are per image and
+identical to batch=1), and under ``torchrun`` the sorted list is split into contiguous shards, one
+per GPU, with the output rows gathered to rank 0 over RCCL (distributed.py).
+"""
+import argparse
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import fmt, models
+
+
+def load_weak_models(model_name: str, model_path: str, num_class: int):
+    """detect.py:15-42.  ``model_path == ""`` asks the reference for downloaded COCO weights; offline
+    this build substitutes seeded synthetic weights of the same architecture (edgeml_amd.synthetic)."""
+    sd = None
+    if model_path != "":
+        ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
+        sd = ckpt["model"] if isinstance(ckpt, dict) and "model" in ckpt and not torch.is_tensor(ckpt["model"]) \
+            else ckpt
+    if model_name == "ssd":
+        if sd is None:
+            return models.ssdlite320_mobilenet_v3_large(weights="DEFAULT", num_classes=num_class)
+        reduced = tuple(sd["backbone.features.1.3.0.weight"].shape)[1] == 80
+        return models.SSDLite320(sd, num_class, reduced)
+    if model_name == "faster_rcnn":
+        if sd is None:
+            return models.fasterrcnn_resnet50_fpn_v2(weights="DEFAULT", num_classes=num_class)
+        return models.FasterRCNNFPNv2(sd, num_class)
+    raise NotImplementedError("retinanet_resnet50_fpn_v2 (detect.py:34-38) is not built yet (SURVEY.md §8f row 3)")
+
+
+def read_image(path):
+    """torchvision.io.read_image(path, ImageReadMode.RGB) -> uint8 [3,H,W] (PIL decoder)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        arr = np.asarray(im.convert("RGB"), dtype=np.uint8)
+    return torch.from_numpy(arr.copy()).permute(2, 0, 1).contiguous()
+
+
+class ObjectDetectionDataset:
+    """detect.py:45-59."""
+
+    def __init__(self, img_dir, names=None):
+        self.img_dir = img_dir
+        self.img_names = sorted(os.listdir(img_dir)) if names is None else list(names)
+
+    def __len__(self):
+        return len(self.img_names)
+
+    def __getitem__(self, idx):
+        image = read_image(os.path.join(self.img_dir, self.img_names[idx]))
+        return image / 255
+
+
+def detect_rows(model, images, dataset="coco"):
+    """Run the engine on a list of [3,H,W] float images; return the .npy rows per image."""
+    preds = model(images)
+    rows = []
+    for img, p in zip(images, preds):
+        rows.append(fmt.format_detections(p["boxes"].cpu().numpy(), p["scores"].cpu().numpy(),
+                                          p["labels"].cpu().numpy(), int(img.shape[-2]), int(img.shape[-1]),
+                                          dataset))
+    return rows
+
+
+def main(opts):
+    from . import distributed as dist_mod
+    img_names = sorted(os.listdir(opts.img_dir))
+    rank, world = dist_mod.rank_world()
+    my_names = dist_mod.shard(img_names, rank, world)
+    dataset = ObjectDetectionDataset(opts.img_dir, my_names)
+    num_class = 91 if opts.dataset == "coco" else 21
+    if not torch.cuda.is_available():
+        raise RuntimeError("edgeml_amd.detect needs an MI355X (HIP) device; there is no CPU path")
+    device = f"cuda:{dist_mod.local_rank()}"
+    torch.cuda.set_device(device)
+    if rank == 0:
+        print(f"Using {device} device (world {world})")
+    model = load_weak_models(opts.model, opts.model_path, num_class).to(device)
+    model.eval()
+    Path(opts.save_dir).mkdir(parents=True, exist_ok=True)
+    batch = getattr(opts, "batch", None) or model.max_batch
+    results = {}
+    pending = []
+
+    def flush():
+        imgs = [im for _, im in pending]
+        for (name, _), r in zip(pending, detect_rows(model, imgs, opts.dataset)):
+            results[name] = r
+        pending.clear()
+
+    for i in range(len(dataset)):
+        img = dataset[i]
+        if pending and (tuple(pending[-1][1].shape) != tuple(img.shape) or len(pending) >= batch):
+            flush()
+        pending.append((my_names[i], img))
+    if pending:
+        flush()
+    if world > 1:
+        results = dist_mod.gather_rows(results, my_names, img_names, rank, world)
+    if rank == 0:
+        for name in img_names:
+            fmt.save_npy(opts.save_dir, name, results[name])
+    return results if rank == 0 else None
+
+
+def getargs(argv=None):
+    """detect.py:109-121 (same positional/optional arguments and defaults) + --batch."""
+    args = argparse.ArgumentParser()
+    args.add_argument('img_dir', help="Directory that saves the image dataset for detection.")
+    args.add_argument('save_dir', help="Directory to save the detection outputs.")
+    args.add_argument('--dataset', type=str, default="coco", help="The dataset to process ('coco' or 'voc').")
+    args.add_argument('--model', type=str, default="ssd",
+                      help="The object detector. Available choices include 'ssd' and 'faster_rcnn'.")
+    args.add_argument("--model-path", type=str, default="",
+                      help="Location of the saved object detection model weights (torchvision state_dict keys).")
+    args.add_argument("--batch", type=int, default=0, help="Images per engine call (0 = model default).")
+    return args.parse_args(argv)
+
+
+if __name__ == '__main__':
+    main(getargs())
+    sys.exit(0)

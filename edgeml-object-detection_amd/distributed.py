@@ -1,0 +1,72 @@
+"""One process per GPU: contiguous shards of the sorted image list and a gather of the output rows.
+
+SURVEY.md §8e: images are independent, so rank r processes the contiguous block
+[r*N//world, (r+1)*N//world) of sorted(os.listdir(img_dir)) (detect.py:64) with no collective on the
+data path.  The only exchange is the final gather of the per-image (n_i, 6) float64 rows to rank 0,
+which writes every file (single writer): an all_gather of per-rank row counts, then an all_gather of
+the packed rows padded to the largest rank (``torch.distributed``; backend "nccl" = RCCL over xGMI on
+the MI355X node, "gloo" in the CPU tests).
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def rank_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def local_rank():
+    return int(os.environ.get("LOCAL_RANK", 0))
+
+
+def shard_bounds(n, rank, world):
+    return rank * n // world, (rank + 1) * n // world
+
+
+def shard(items, rank, world):
+    lo, hi = shard_bounds(len(items), rank, world)
+    return list(items)[lo:hi]
+
+
+def gather_rows(results, my_names, all_names, rank, world, device=None):
+    """results: {name: (n,6) float64} for this rank's shard -> {name: rows} for every image on rank 0."""
+    if world == 1:
+        return results
+    if not dist.is_initialized():
+        raise RuntimeError("gather_rows needs an initialised torch.distributed process group")
+    backend = dist.get_backend()
+    dev = device or (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu"))
+    counts = np.asarray([results[n].shape[0] for n in my_names], dtype=np.int64)
+    rows = np.concatenate([results[n].reshape(-1, 6) for n in my_names], 0) if my_names else np.zeros((0, 6))
+    meta = torch.tensor([len(my_names), rows.shape[0]], dtype=torch.int64, device=dev)
+    metas = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta)
+    metas = [m.cpu().tolist() for m in metas]
+    max_imgs = max(m[0] for m in metas)
+    max_rows = max(m[1] for m in metas)
+    c = torch.zeros(max(max_imgs, 1), dtype=torch.int64, device=dev)
+    c[:len(counts)] = torch.from_numpy(counts).to(dev)
+    r = torch.zeros((max(max_rows, 1), 6), dtype=torch.float64, device=dev)
+    r[:rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.float64)).to(dev)
+    cs = [torch.zeros_like(c) for _ in range(world)]
+    rs = [torch.zeros_like(r) for _ in range(world)]
+    dist.all_gather(cs, c)
+    dist.all_gather(rs, r)
+    if rank != 0:
+        return None
+    out = {}
+    for k in range(world):
+        lo, hi = shard_bounds(len(all_names), k, world)
+        names = all_names[lo:hi]
+        cnt = cs[k].cpu().numpy()[:len(names)]
+        rr = rs[k].cpu().numpy()
+        pos = 0
+        for name, n in zip(names, cnt):
+            out[name] = rr[pos:pos + n].copy().reshape(int(n), 6)
+            pos += int(n)
+    return out

@@ -1,0 +1,553 @@
+"""The two detectors of torch_models/detect.py, lowered onto libedgedet.so.
+
+``SSDLite320`` restates torchvision's ``ssdlite320_mobilenet_v3_large`` (detect.py:24/26) and
+``FasterRCNNFPNv2`` restates ``fasterrcnn_resnet50_fpn_v2`` (detect.py:30/32).  Both keep
+torchvision's detection-model contract (detect.py:72-81): ``.to(device)``, ``.eval()``,
+``.load_state_dict(sd)`` with torchvision's state_dict keys, and
+``model(Tensor[N,3,H,W] float32 in [0,1]) -> [{"boxes", "scores", "labels"}]`` with boxes in original
+pixels, scores descending, labels int64.  Every arithmetic step runs in HIP kernels (plan.py lowers
+the forward into one op list per input shape; ops.py loads the library and fails loudly if it is
+missing).  Architecture and post-processing constants: SURVEY.md Appendix A.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import anchors as anc
+from . import arch
+from . import ops
+from .plan import Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight
+
+
+def _np(t):
+    return t.detach().cpu().to(torch.float64).numpy()
+
+
+def _check_keys(sd, table, what):
+    missing = [k for k in table if k not in sd]
+    unexpected = [k for k in sd if k not in table]
+    bad = [k for k in table if k in sd and tuple(sd[k].shape) != tuple(table[k])]
+    if missing or unexpected or bad:
+        raise RuntimeError(f"Error(s) in loading state_dict for {what}: missing keys {missing[:5]}, "
+                           f"unexpected keys {unexpected[:5]}, size mismatch {bad[:5]}")
+
+
+class _Detector:
+    kind = None
+    max_batch = 32
+
+    def __init__(self, state_dict, num_classes=91, device=None):
+        self.num_classes = num_classes
+        self.device = torch.device(device) if device is not None else None
+        self.training = False
+        self.plans = {}
+        self.load_state_dict(state_dict)
+
+    # torchvision-style surface ----------------------------------------------------------------
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("training is out of scope (SURVEY.md §2 row 7)")
+        return self
+
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError(f"{type(self).__name__} runs on the MI355X HIP engine only (got {device}); "
+                               f"there is no CPU fallback")
+        self.device = device
+        return self
+
+    def cuda(self):
+        return self.to("cuda")
+
+    def load_state_dict(self, sd, strict=True):
+        sd = {k: v for k, v in sd.items()}
+        _check_keys(sd, self.table(), type(self).__name__)
+        self.sd = sd
+        self.pack = WeightPack()
+        self._w = {}
+        self._pack_all()
+        self.plans = {}
+        return self
+
+    def state_dict(self):
+        return dict(self.sd)
+
+    # weights ----------------------------------------------------------------------------------
+    def _conv_bn(self, wkey, bnp, eps, cin_pad=None):
+        """(w, b, K, Kpad, Cin) of a bias-free conv followed by BatchNorm prefix `bnp`."""
+        key = ("cbn", wkey)
+        if key not in self._w:
+            s = self.sd
+            wf, bf = fold_bn(_np(s[wkey]), _np(s[bnp + ".weight"]), _np(s[bnp + ".bias"]),
+                             _np(s[bnp + ".running_mean"]), _np(s[bnp + ".running_var"]), eps)
+            if wf.shape[1] == 1 and wf.shape[0] > 1 and cin_pad is None and self._is_dw(wkey):
+                self._w[key] = (self.pack.add(pack_dw_weight(wf)), self.pack.add(bf), wf.shape[-1], None, wf.shape[0])
+            else:
+                wp, K, Kpad, cin = pack_conv_weight(wf, cin_pad)
+                self._w[key] = (self.pack.add(wp), self.pack.add(bf), K, Kpad, cin)
+        return self._w[key]
+
+    def _conv_bias(self, wkey, bkey, perm=None):
+        key = ("cb", wkey)
+        if key not in self._w:
+            w = _np(self.sd[wkey]).astype(np.float32)
+            b = _np(self.sd[bkey]).astype(np.float32)
+            if w.ndim == 2:
+                w = w[:, :, None, None]
+            wp, K, Kpad, cin = pack_conv_weight(w)
+            self._w[key] = (self.pack.add(wp), self.pack.add(b), K, Kpad, cin)
+        return self._w[key]
+
+    def _is_dw(self, wkey):
+        return False
+
+    # inference --------------------------------------------------------------------------------
+    def plan(self, B, H, W):
+        key = (int(B), int(H), int(W))
+        if key not in self.plans:
+            if self.device is None:
+                self.to("cuda")
+            self.plans[key] = self.build_plan(*key).finalize()
+        return self.plans[key]
+
+    @torch.no_grad()
+    def __call__(self, images):
+        if self.device is None:
+            self.to("cuda")
+        imgs = list(images) if not torch.is_tensor(images) or images.dim() == 3 else list(images.unbind(0))
+        if torch.is_tensor(images) and images.dim() == 3:
+            imgs = [images]
+        results = [None] * len(imgs)
+        groups = {}
+        for idx, im in enumerate(imgs):
+            groups.setdefault(tuple(im.shape[-2:]), []).append(idx)
+        for (H, W), idxs in groups.items():
+            for s in range(0, len(idxs), self.max_batch):
+                chunk = idxs[s:s + self.max_batch]
+                plan = self.plan(len(chunk), H, W)
+                inp = plan.input.tensor()
+                for j, idx in enumerate(chunk):
+                    inp[j].copy_(imgs[idx].to(self.device, torch.float32), non_blocking=True)
+                plan.run()
+                counts = plan.out_count.tensor().cpu().tolist()
+                boxes = plan.out_box.tensor()
+                scores = plan.out_score.tensor()
+                labels = plan.out_label.tensor()
+                for j, idx in enumerate(chunk):
+                    n = counts[j]
+                    results[idx] = {"boxes": boxes[j, :n].clone(), "scores": scores[j, :n].clone(),
+                                    "labels": labels[j, :n].clone()}
+        return results
+
+    forward = __call__
+
+
+# ====================================================================================== SSDLite
+class SSDLite320(_Detector):
+    """ssdlite320_mobilenet_v3_large."""
+
+    kind = "ssd"
+    BN_EPS = 1e-3
+    SIZE = 320
+    SCORE_THRESH, NMS_THRESH, DETS, TOPK = 0.001, 0.55, 300, 300
+    max_batch = 64
+
+    def __init__(self, state_dict, num_classes=91, reduced_tail=None, device=None):
+        if reduced_tail is None:
+            reduced_tail = tuple(state_dict["backbone.features.1.3.0.weight"].shape)[1] == 80
+        self.reduced_tail = reduced_tail
+        super().__init__(state_dict, num_classes, device)
+
+    def table(self):
+        return arch.ssdlite_table(self.num_classes, self.reduced_tail)
+
+    def _is_dw(self, wkey):
+        return tuple(self.sd[wkey].shape)[1] == 1 and tuple(self.sd[wkey].shape)[0] > 1
+
+    def _pack_all(self):
+        # pack eagerly in network order so the blob is laid out like the forward walks it
+        self.build_plan(1, self.SIZE, self.SIZE, pack_only=True)
+
+    def _se(self, p):
+        key = ("se", p)
+        if key not in self._w:
+            w1 = _np(self.sd[p + ".fc1.weight"])[:, :, 0, 0]  # [S, C]
+            w2 = _np(self.sd[p + ".fc2.weight"])[:, :, 0, 0]  # [C, S]
+            self._w[key] = (self.pack.add(w1.T), self.pack.add(_np(self.sd[p + ".fc1.bias"])),
+                            self.pack.add(w2.T), self.pack.add(_np(self.sd[p + ".fc2.bias"])), w1.shape[0])
+        return self._w[key]
+
+    def build_plan(self, B, H, W, pack_only=False):
+        P = Plan(self.pack, self.device or "cpu")
+        NC = self.num_classes
+        S = self.SIZE
+        inp = P.buf((B, 3, H, W), name="images")
+        x = P.buf((B, S, S, 4), name="pre")
+        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {0: inp, 1: x},
+                 {0: 0.5, 1: 0.5, 2: 0.5, 3: 0.5, 4: 0.5, 5: 0.5}, name="transform"))
+        cur = (x, (B, S, S, 4))
+
+        def conv(cur, prefix, k, stride, act, res=None, in_scale=None, cin_pad=None):
+            xb, xs = cur
+            w, b, K, Kpad, cin = self._conv_bn(prefix + ".0.weight", prefix + ".1", self.BN_EPS, cin_pad)
+            cout = int(self.sd[prefix + ".0.weight"].shape[0])
+            Ho = (xs[1] + 2 * ((k - 1) // 2) - k) // stride + 1
+            Wo = (xs[2] + 2 * ((k - 1) // 2) - k) // stride + 1
+            ys = (B, Ho, Wo, cout)
+            y = P.buf(ys, name=prefix)
+            conv_op(P, xb, xs, w, b, cout, k, stride, (k - 1) // 2, act, y, ys, K, Kpad, res=res,
+                    in_scale=in_scale, name=prefix)
+            return (y, ys)
+
+        def dw(cur, prefix, k, stride, act):
+            xb, xs = cur
+            w, b, _, _, c = self._conv_bn(prefix + ".0.weight", prefix + ".1", self.BN_EPS)
+            pad = (k - 1) // 2
+            Ho = (xs[1] + 2 * pad - k) // stride + 1
+            Wo = (xs[2] + 2 * pad - k) // stride + 1
+            ys = (B, Ho, Wo, xs[3])
+            y = P.buf(ys, name=prefix)
+            P.add(Op(ops.DWCONV, {0: B, 1: xs[1], 2: xs[2], 3: xs[3], 4: Ho, 5: Wo, 6: k, 7: stride, 8: pad,
+                                  9: ops.ACT[act]}, {0: xb, 1: w, 2: b, 3: y}, name=prefix))
+            return (y, ys)
+
+        def se(cur, p):
+            xb, xs = cur
+            w1t, b1, w2t, b2, sq = self._se(p)
+            C = xs[3]
+            mean = P.buf((B, C), name=p + ".mean")
+            scale = P.buf((B, C), name=p + ".scale")
+            P.add(Op(ops.CHANNEL_MEAN, {0: B, 1: xs[1] * xs[2], 2: C}, {0: xb, 1: mean}, name=p + ".avgpool"))
+            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq}, {0: mean, 1: w1t, 2: b1, 3: w2t, 4: b2, 5: scale}, name=p))
+            return scale
+
+        def inverted_residual(cur, cnf, base):
+            cin, k, exp, cout, use_se, act, stride = cnf
+            pe, pd, ps, pp = arch.block_prefixes(cnf, base)
+            y = cur
+            if pe:
+                y = conv(y, pe, 1, 1, act)
+            y = dw(y, pd, k, stride, act)
+            scale = se(y, ps) if use_se else None
+            res = cur[0] if (stride == 1 and cin == cout) else None
+            return conv(y, pp, 1, 1, None, res=res, in_scale=scale)
+
+        cfg = arch.mnv3_blocks(self.reduced_tail)
+        cur = conv(cur, "backbone.features.0.0", 3, 2, "HS", cin_pad=4)
+        for i in range(12):
+            cur = inverted_residual(cur, cfg[i], f"backbone.features.0.{i + 1}.block")
+        _, k, exp, cout, _, act, stride = cfg[12]
+        cur = conv(cur, "backbone.features.0.13", 1, 1, act)
+        feats = [cur]
+        y = dw(cur, "backbone.features.1.0.1", k, stride, act)
+        scale = se(y, "backbone.features.1.0.2")
+        cur = conv(y, "backbone.features.1.0.3", 1, 1, None, in_scale=scale)
+        for i in (13, 14):
+            cur = inverted_residual(cur, cfg[i], f"backbone.features.1.{i - 12}.block")
+        cur = conv(cur, "backbone.features.1.3", 1, 1, "HS")
+        feats.append(cur)
+        for e in range(4):
+            p = f"backbone.extra.{e}"
+            cur = conv(cur, p + ".0", 1, 1, "R6")
+            cur = dw(cur, p + ".1", 3, 2, "R6")
+            cur = conv(cur, p + ".2", 1, 1, "R6")
+            feats.append(cur)
+
+        grids = [(f[1][1], f[1][2]) for f in feats]
+        A = sum(h * w * 6 for h, w in grids)
+        cls = P.buf((B, A, NC), name="cls_logits")
+        reg = P.buf((B, A, 4), name="bbox_regression")
+        off = 0
+        for i, f in enumerate(feats):
+            fb, fs = f
+            for name, cols, out in (("classification_head", NC, cls), ("regression_head", 4, reg)):
+                p = f"head.{name}.module_list.{i}"
+                t = dw(f, p + ".0", 3, 1, "R6")
+                w, b, K, Kpad, cin = self._conv_bias(p + ".1.weight", p + ".1.bias")
+                cout = 6 * cols
+                conv_op(P, t[0], t[1], w, b, cout, 1, 1, 0, None, out, (B, fs[1], fs[2], cout), K, Kpad,
+                        y_pstride=cout, y_bstride=A * cols, y_off=off * cols, name=p + ".1")
+            off += fs[1] * fs[2] * 6
+        self.grids = grids
+        if pack_only:
+            return P
+
+        anchors = P.const(anc.ssd_default_boxes(grids, (S, S)), name="anchors")
+        scores_t = P.buf((B, NC, A), name="scores_t")
+        boxes = P.buf((B, A, 4), name="boxes")
+        P.add(Op(ops.SSD_SCORES, {0: B, 1: A, 2: NC}, {0: cls, 1: reg, 2: anchors, 3: scores_t, 4: boxes},
+                 {0: S, 1: S}, name="postprocess.scores"))
+        NS, KM = NC - 1, self.TOPK
+        rec = [P.buf((B, NS, KM, 4), name="rec.box"), P.buf((B, NS, KM), name="rec.score"),
+               P.buf((B, NS, KM), torch.int32, name="rec.tb"), P.buf((B, NS, KM), torch.int32, name="rec.label"),
+               P.buf((B, NS), torch.int32, name="rec.count")]
+        P.add(Op(ops.SSD_CLASS_NMS, {0: B, 1: A, 2: NC, 3: self.TOPK, 4: KM},
+                 {0: scores_t, 1: boxes, 2: rec[0], 3: rec[1], 4: rec[2], 5: rec[3], 6: rec[4]},
+                 {0: self.SCORE_THRESH}, {0: self.NMS_THRESH}, name="postprocess.class_nms"))
+        ratio = np.tile(np.asarray([np.float32(W) / np.float32(S), np.float32(H) / np.float32(S)], np.float32),
+                        (B, 1))
+        ratio_b = P.const(ratio, name="ratio")
+        P.out_box = P.buf((B, self.DETS, 4), name="out.boxes")
+        P.out_score = P.buf((B, self.DETS), name="out.scores")
+        P.out_label = P.buf((B, self.DETS), torch.int64, name="out.labels")
+        P.out_count = P.buf((B,), torch.int32, name="out.count")
+        P.add(Op(ops.MERGE_TOPK, {0: B, 1: NS, 2: KM, 3: self.DETS},
+                 {0: rec[0], 1: rec[1], 2: rec[2], 3: rec[3], 4: rec[4], 5: ratio_b, 6: P.out_box, 7: P.out_score,
+                  8: P.out_label, 9: P.out_count}, name="postprocess.merge"))
+        P.input = inp
+        P.cls_logits, P.bbox_regression = cls, reg
+        P.feats = [f[0] for f in feats]
+        return P
+
+
+# ====================================================================================== FRCNN
+class FasterRCNNFPNv2(_Detector):
+    """fasterrcnn_resnet50_fpn_v2."""
+
+    kind = "faster_rcnn"
+    BN_EPS = 1e-5
+    MEAN = (0.485, 0.456, 0.406)
+    STD = (0.229, 0.224, 0.225)
+    MIN_SIZE, MAX_SIZE, DIVISIBLE = 800, 1333, 32
+    RPN_PRE, RPN_POST, RPN_NMS, RPN_MIN, RPN_SCORE = 1000, 1000, 0.7, 1e-3, 0.0
+    BOX_SCORE, BOX_NMS, BOX_DETS, BOX_MIN = 0.05, 0.5, 100, 1e-2
+    max_batch = 8
+
+    def table(self):
+        return arch.frcnn_table(self.num_classes)
+
+    def _pack_all(self):
+        self.build_plan(1, self.MIN_SIZE, self.MIN_SIZE, pack_only=True)
+
+    def _fc6(self):
+        key = ("fc6",)
+        if key not in self._w:
+            w = _np(self.sd["roi_heads.box_head.5.weight"]).astype(np.float32)  # [1024, 256*7*7] (c, h, w)
+            w = w.reshape(-1, 256, 7, 7).transpose(0, 2, 3, 1).reshape(w.shape[0], -1)  # -> (h, w, c)
+            b = _np(self.sd["roi_heads.box_head.5.bias"]).astype(np.float32)
+            wp, K, Kpad, cin = pack_conv_weight(w[:, :, None, None])
+            self._w[key] = (self.pack.add(wp), self.pack.add(b), K, Kpad, cin)
+        return self._w[key]
+
+    def _predictor(self):
+        key = ("pred",)
+        if key not in self._w:
+            q = "roi_heads.box_predictor."
+            w = np.concatenate([_np(self.sd[q + "bbox_pred.weight"]), _np(self.sd[q + "cls_score.weight"])], 0)
+            b = np.concatenate([_np(self.sd[q + "bbox_pred.bias"]), _np(self.sd[q + "cls_score.bias"])], 0)
+            wp, K, Kpad, cin = pack_conv_weight(w.astype(np.float32)[:, :, None, None])
+            self._w[key] = (self.pack.add(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
+        return self._w[key]
+
+    def _rpn_out(self):
+        key = ("rpn_out",)
+        if key not in self._w:
+            p = "rpn.head."
+            w = np.concatenate([_np(self.sd[p + "cls_logits.weight"]), _np(self.sd[p + "bbox_pred.weight"])], 0)
+            b = np.concatenate([_np(self.sd[p + "cls_logits.bias"]), _np(self.sd[p + "bbox_pred.bias"])], 0)
+            wp, K, Kpad, cin = pack_conv_weight(w.astype(np.float32))
+            self._w[key] = (self.pack.add(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
+        return self._w[key]
+
+    def resized_size(self, H, W):
+        scale = min(float(self.MIN_SIZE) / min(H, W), float(self.MAX_SIZE) / max(H, W))
+        return int(math.floor(H * scale)), int(math.floor(W * scale))
+
+    def build_plan(self, B, H, W, pack_only=False):
+        P = Plan(self.pack, self.device or "cpu")
+        NC = self.num_classes
+        Ho, Wo = self.resized_size(H, W)
+        Hp = (Ho + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
+        Wp = (Wo + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
+        inp = P.buf((B, 3, H, W), name="images")
+        x = P.buf((B, Hp, Wp, 4), name="pre")
+        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: Ho, 4: Wo, 5: Hp, 6: Wp}, {0: inp, 1: x},
+                 {0: self.MEAN[0], 1: self.MEAN[1], 2: self.MEAN[2], 3: self.STD[0], 4: self.STD[1],
+                  5: self.STD[2]}, name="transform"))
+        cur = (x, (B, Hp, Wp, 4))
+
+        def conv(cur, wkey, bnp, k, stride, act, res=None, res_hw=None, cin_pad=None, bias_key=None, name=None,
+                 tile=0):
+            xb, xs = cur
+            if bias_key is not None:
+                w, b, K, Kpad, cin = self._conv_bias(wkey, bias_key)
+            else:
+                w, b, K, Kpad, cin = self._conv_bn(wkey, bnp, self.BN_EPS, cin_pad)
+            cout = int(self.sd[wkey].shape[0])
+            pad = (k - 1) // 2
+            Ho_ = (xs[1] + 2 * pad - k) // stride + 1
+            Wo_ = (xs[2] + 2 * pad - k) // stride + 1
+            ys = (xs[0], Ho_, Wo_, cout)
+            y = P.buf(ys, name=name or wkey)
+            conv_op(P, xb, xs, w, b, cout, k, stride, pad, act, y, ys, K, Kpad, res=res, res_hw=res_hw,
+                    name=name or wkey, tile=tile)
+            return (y, ys)
+
+        def maxpool(cur, k, stride, pad, name):
+            xb, xs = cur
+            Ho_ = (xs[1] + 2 * pad - k) // stride + 1
+            Wo_ = (xs[2] + 2 * pad - k) // stride + 1
+            ys = (xs[0], Ho_, Wo_, xs[3])
+            y = P.buf(ys, name=name)
+            P.add(Op(ops.MAXPOOL, {0: xs[0], 1: xs[1], 2: xs[2], 3: xs[3], 4: Ho_, 5: Wo_, 6: k, 7: stride, 8: pad},
+                     {0: xb, 1: y}, name=name))
+            return (y, ys)
+
+        # ---- ResNet-50 body
+        p = "backbone.body."
+        cur = conv(cur, p + "conv1.weight", p + "bn1", 7, 2, "RE", cin_pad=4)
+        cur = maxpool(cur, 3, 2, 1, "backbone.body.maxpool")
+        cs = []
+        for lname, nblk, width, stride in arch.RESNET_LAYERS:
+            for bi in range(nblk):
+                q = f"{p}{lname}.{bi}."
+                s = stride if bi == 0 else 1
+                y = conv(cur, q + "conv1.weight", q + "bn1", 1, 1, "RE")
+                y = conv(y, q + "conv2.weight", q + "bn2", 3, s, "RE")
+                if bi == 0:
+                    idn = conv(cur, q + "downsample.0.weight", q + "downsample.1", 1, s, None)
+                else:
+                    idn = cur
+                cur = conv(y, q + "conv3.weight", q + "bn3", 1, 1, "RE", res=idn[0])
+            cs.append(cur)
+
+        # ---- FPN (BN, no activations) + LastLevelMaxPool
+        f = "backbone.fpn."
+        last = conv(cs[3], f + "inner_blocks.3.0.weight", f + "inner_blocks.3.1", 1, 1, None)
+        outs = [conv(last, f + "layer_blocks.3.0.weight", f + "layer_blocks.3.1", 3, 1, None)]
+        for i in (2, 1, 0):
+            last = conv(cs[i], f"{f}inner_blocks.{i}.0.weight", f"{f}inner_blocks.{i}.1", 1, 1, None,
+                        res=last[0], res_hw=(last[1][1], last[1][2]))
+            outs.insert(0, conv(last, f"{f}layer_blocks.{i}.0.weight", f"{f}layer_blocks.{i}.1", 3, 1, None))
+        outs.append(maxpool(outs[-1], 1, 2, 0, "backbone.fpn.extra_blocks.pool"))
+        if pack_only:
+            for k in ("rpn.head.conv.0.0", "rpn.head.conv.1.0"):
+                self._conv_bias(k + ".weight", k + ".bias")
+            self._rpn_out()
+            for i in range(4):
+                self._conv_bn(f"roi_heads.box_head.{i}.0.weight", f"roi_heads.box_head.{i}.1", self.BN_EPS)
+            self._fc6()
+            self._predictor()
+            return P
+
+        # ---- RPN head (shared over levels) + proposal filtering
+        A = 3
+        heads, grids = [], []
+        for lvl, fm in enumerate(outs):
+            t = conv(fm, "rpn.head.conv.0.0.weight", None, 3, 1, "RE", bias_key="rpn.head.conv.0.0.bias",
+                     name=f"rpn.head.conv.0@{lvl}")
+            t = conv(t, "rpn.head.conv.1.0.weight", None, 3, 1, "RE", bias_key="rpn.head.conv.1.0.bias",
+                     name=f"rpn.head.conv.1@{lvl}")
+            w, b, K, Kpad, cin = self._rpn_out()
+            hs = (B, fm[1][1], fm[1][2], 15)
+            hb = P.buf(hs, name=f"rpn.head.out@{lvl}")
+            conv_op(P, t[0], t[1], w, b, 15, 1, 1, 0, None, hb, hs, K, Kpad, name=f"rpn.head.cls_bbox@{lvl}")
+            heads.append(hb)
+            grids.append((fm[1][1], fm[1][2]))
+        anchor_bufs = [P.const(a, name=f"rpn.anchors@{l}") for l, a in enumerate(anc.rpn_anchors(grids, (Hp, Wp)))]
+        L = len(outs)
+        KM = self.RPN_PRE
+        rrec = [P.buf((B, L, KM, 4), name="rpn.rec.box"), P.buf((B, L, KM), name="rpn.rec.score"),
+                P.buf((B, L, KM), torch.int32, name="rpn.rec.tb"), P.buf((B, L, KM), torch.int32, name="rpn.rec.lvl"),
+                P.buf((B, L), torch.int32, name="rpn.rec.count")]
+        pi = {0: B, 1: L, 2: 15, 3: A, 4: self.RPN_PRE, 5: KM}
+        pp = {}
+        for l in range(L):
+            pi[6 + l] = grids[l][0] * grids[l][1] * A
+            pp[l] = heads[l]
+            pp[5 + l] = anchor_bufs[l]
+        for j in range(5):
+            pp[10 + j] = rrec[j]
+        P.add(Op(ops.RPN_LEVEL_NMS, pi, pp, {0: Ho, 1: Wo, 2: self.RPN_MIN, 3: self.RPN_SCORE}, {0: self.RPN_NMS},
+                 name="rpn.filter_proposals"))
+        R = self.RPN_POST
+        props = P.buf((B, R, 4), name="proposals")
+        pscore = P.buf((B, R), name="proposal_scores")
+        pcount = P.buf((B,), torch.int32, name="proposal_count")
+        P.add(Op(ops.MERGE_TOPK, {0: B, 1: L, 2: KM, 3: R},
+                 {0: rrec[0], 1: rrec[1], 2: rrec[2], 3: rrec[3], 4: rrec[4], 5: None, 6: props, 7: pscore, 8: None,
+                  9: pcount}, name="rpn.post_nms_top_n"))
+
+        # ---- MultiScaleRoIAlign (levels '0'..'3')
+        C = 256
+        roi = P.buf((B * R, 7, 7, C), name="box_roi_pool")
+        ri = {0: 1, 1: B * R, 2: R, 3: B, 4: C, 5: 7, 6: 7, 7: 2, 8: 4, 9: 2, 10: 5}
+        rp = {4: props, 5: pcount, 6: roi}
+        rf = {}
+        for l in range(4):
+            fh, fw = outs[l][1][1], outs[l][1][2]
+            ri[11 + l], ri[15 + l] = fh, fw
+            rp[l] = outs[l][0]
+            # MultiScaleRoIAlign._infer_scale: 2 ** round(log2(feat / image)) in float32
+            rf[l] = 2.0 ** float(torch.tensor(float(fh) / float(Ho)).log2().round())
+        P.add(Op(ops.ROI_ALIGN, ri, rp, rf, name="roi_heads.box_roi_pool"))
+
+        # ---- box head + predictor
+        cur = (roi, (B * R, 7, 7, C))
+        for i in range(4):
+            cur = conv(cur, f"roi_heads.box_head.{i}.0.weight", f"roi_heads.box_head.{i}.1", 3, 1, "RE")
+        w, b, K, Kpad, cin = self._fc6()
+        fc6 = P.buf((B * R, 1024), name="roi_heads.box_head.5")
+        conv_op(P, cur[0], (B * R, 1, 1, 7 * 7 * C), w, b, 1024, 1, 1, 0, "RE", fc6, (B * R, 1, 1, 1024), K, Kpad,
+                name="roi_heads.box_head.5")
+        w, b, K, Kpad, cin = self._predictor()
+        LD = 456
+        pred = P.buf((B * R, LD), name="box_predictor")
+        conv_op(P, fc6, (B * R, 1, 1, 1024), w, b, 5 * NC, 1, 1, 0, None, pred, (B * R, 1, 1, 5 * NC), K, Kpad,
+                y_pstride=LD, y_bstride=LD, name="roi_heads.box_predictor")
+
+        # ---- RoIHeads.postprocess_detections
+        scores = P.buf((B, R, NC), name="box_scores")
+        bxs = P.buf((B, R, NC, 4), name="box_decoded")
+        P.add(Op(ops.BOX_SCORES, {0: LD, 1: B, 2: R, 3: NC, 4: 4 * NC, 5: 0}, {0: pred, 1: props, 2: pcount,
+                                                                             3: scores, 4: bxs},
+                 {0: Ho, 1: Wo}, name="roi_heads.scores_decode"))
+        NS = NC - 1
+        brec = [P.buf((B, NS, R, 4), name="box.rec.box"), P.buf((B, NS, R), name="box.rec.score"),
+                P.buf((B, NS, R), torch.int32, name="box.rec.tb"), P.buf((B, NS, R), torch.int32, name="box.rec.lbl"),
+                P.buf((B, NS), torch.int32, name="box.rec.count")]
+        P.add(Op(ops.BOX_CLASS_NMS, {0: B, 1: R, 2: NC, 3: R},
+                 {0: scores, 1: bxs, 2: pcount, 3: brec[0], 4: brec[1], 5: brec[2], 6: brec[3], 7: brec[4]},
+                 {0: self.BOX_SCORE, 1: self.BOX_MIN}, {0: self.BOX_NMS}, name="roi_heads.class_nms"))
+        ratio = np.tile(np.asarray([np.float32(W) / np.float32(Wo), np.float32(H) / np.float32(Ho)], np.float32),
+                        (B, 1))
+        ratio_b = P.const(ratio, name="ratio")
+        N = self.BOX_DETS
+        P.out_box = P.buf((B, N, 4), name="out.boxes")
+        P.out_score = P.buf((B, N), name="out.scores")
+        P.out_label = P.buf((B, N), torch.int64, name="out.labels")
+        P.out_count = P.buf((B,), torch.int32, name="out.count")
+        P.add(Op(ops.MERGE_TOPK, {0: B, 1: NS, 2: R, 3: N},
+                 {0: brec[0], 1: brec[1], 2: brec[2], 3: brec[3], 4: brec[4], 5: ratio_b, 6: P.out_box,
+                  7: P.out_score, 8: P.out_label, 9: P.out_count}, name="roi_heads.detections_per_img"))
+        P.input = inp
+        P.feats = [o[0] for o in outs]
+        P.proposals, P.proposal_count = props, pcount
+        P.box_features = roi
+        P.pred = pred
+        return P
+
+
+# ====================================================================================== factories
+def ssdlite320_mobilenet_v3_large(weights=None, num_classes=91, reduced_tail=True, state_dict=None, seed=0):
+    """Builder mirroring torchvision's (detect.py:24,26).  ``weights="DEFAULT"`` would download COCO
+    weights, impossible offline: pass ``state_dict=`` (e.g. torch.load(--model-path)) or get seeded
+    synthetic weights (edgeml_amd.synthetic) in their place."""
+    from . import synthetic
+    if state_dict is None:
+        state_dict = synthetic.synthetic_state_dict("ssd", num_classes, reduced_tail, seed=seed)
+    return SSDLite320(state_dict, num_classes, reduced_tail)
+
+
+def fasterrcnn_resnet50_fpn_v2(weights=None, num_classes=91, state_dict=None, seed=0):
+    """Builder mirroring torchvision's (detect.py:30,32); see ssdlite320_mobilenet_v3_large."""
+    from . import synthetic
+    if state_dict is None:
+        state_dict = synthetic.synthetic_state_dict("faster_rcnn", num_classes, seed=seed)
+    return FasterRCNNFPNv2(state_dict, num_classes)

@@ -1,0 +1,150 @@
+"""ctypes binding of libedgedet.so (the C-ABI declared in include/edgedet.h).
+
+Importing this module never falls back to anything: if the library is missing or cannot be loaded
+the import-time helper ``lib()`` raises ``EdgeDetUnavailable``.  ``torch`` is imported first so the
+library binds to the same HIP runtime (libamdhip64.so.7) that PyTorch-ROCm already loaded, and
+device pointers / streams from torch tensors are valid inside the library.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch  # noqa: F401  (must precede loading libedgedet.so: shared HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libedgedet.so")
+
+OP_INTS, OP_PTRS, OP_DBLS, OP_FLTS = 48, 24, 8, 16
+
+# kinds (include/edgedet.h)
+MEMSET, PREPROCESS, CONV, DWCONV, CHANNEL_MEAN, SE_FC, MAXPOOL = 1, 2, 3, 4, 5, 6, 7
+SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX_CLASS_NMS = 8, 9, 10, 11, 12, 13, 14
+
+# activations (csrc/common.hpp)
+ACT = {None: 0, "RE": 1, "R6": 2, "HS": 3, "HSIG": 4, "SIG": 5}
+
+OP_DTYPE = np.dtype([("kind", "<i8"), ("i", "<i8", OP_INTS), ("p", "<u8", OP_PTRS), ("d", "<f8", OP_DBLS),
+                     ("f", "<f4", OP_FLTS)])
+assert OP_DTYPE.itemsize == 8 + 8 * OP_INTS + 8 * OP_PTRS + 8 * OP_DBLS + 4 * OP_FLTS
+
+EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
+           "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
+           "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target")
+
+
+class EdgeDetUnavailable(RuntimeError):
+    pass
+
+
+class EdgeDetError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+_vp, _i64, _i32, _dbl, _flt = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
+
+
+def lib():
+    """Load libedgedet.so once (raises EdgeDetUnavailable when it is not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise EdgeDetUnavailable(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                                 f"(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise EdgeDetUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    L.edgedet_plan_run.argtypes = [_vp, _i64, _vp]
+    L.edgedet_graph_create.argtypes = [_vp, _i64, _vp, ctypes.POINTER(_vp)]
+    L.edgedet_graph_launch.argtypes = [_vp, _vp]
+    L.edgedet_graph_destroy.argtypes = [_vp]
+    L.edgedet_nms.argtypes = [_vp, _vp, _i64, _dbl, _vp, _vp, _vp]
+    L.edgedet_batched_nms.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp]
+    L.edgedet_roi_align.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _flt, _i32, _i32, _i32, _vp, _vp]
+    L.edgedet_conv2d.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
+                                 _vp, _vp]
+    L.edgedet_conv_weight_k.argtypes = [_i32, _i32, _i64]
+    L.edgedet_conv_weight_k.restype = _i64
+    L.edgedet_dwconv2d.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]
+    L.edgedet_last_error.restype = ctypes.c_char_p
+    L.edgedet_version.restype = _i32
+    L.edgedet_target.restype = ctypes.c_char_p
+    for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
+                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d"):
+        getattr(L, name).restype = ctypes.c_int
+    _LIB = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise EdgeDetError(f"libedgedet error {rc}: {lib().edgedet_last_error().decode()}")
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or not t.is_contiguous()):
+            raise ValueError("libedgedet operators take contiguous device tensors")
+
+
+# ------------------------------------------------------------------------------ unit operators
+def nms(boxes, scores, iou_threshold):
+    """torchvision.ops.nms on the device (boxes [n,4] f32, scores [n] f32) -> int64 keep indices."""
+    return batched_nms(boxes, scores, None, iou_threshold)
+
+
+def batched_nms(boxes, scores, idxs, iou_threshold):
+    """torchvision.ops.batched_nms on the device; result sorted by score desc, ties lower index."""
+    _need_cuda(boxes, scores, idxs)
+    n = int(scores.shape[0])
+    keep = torch.empty(max(n, 1), dtype=torch.int64, device=scores.device)
+    nk = torch.zeros(1, dtype=torch.int32, device=scores.device)
+    check(lib().edgedet_batched_nms(_ptr(boxes), _ptr(scores), _ptr(idxs), n, float(iou_threshold), _ptr(keep),
+                                    _ptr(nk), stream_handle()))
+    return keep[:int(nk.item())]
+
+
+def roi_align_nhwc(feat_nhwc, rois, spatial_scale, output_size=7, sampling_ratio=2):
+    """torchvision.ops.roi_align(aligned=False) on an NHWC map; returns [R, PH, PW, C]."""
+    _need_cuda(feat_nhwc, rois)
+    B, H, W, C = feat_nhwc.shape
+    R = rois.shape[0]
+    out = torch.empty((R, output_size, output_size, C), dtype=torch.float32, device=feat_nhwc.device)
+    check(lib().edgedet_roi_align(_ptr(feat_nhwc), B, H, W, C, _ptr(rois), R, float(spatial_scale), output_size,
+                                  output_size, sampling_ratio, _ptr(out), stream_handle()))
+    return out
+
+
+def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None):
+    """Fused conv (+ folded BN) + residual + activation on NHWC; w_packed from pack_conv_weight."""
+    _need_cuda(x, w_packed, bias, res)
+    B, H, W, Cin = x.shape
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
+    check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad, ACT[act],
+                               _ptr(res), _ptr(y), stream_handle()))
+    return y
+
+
+def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None):
+    _need_cuda(x, w_taps, bias)
+    B, H, W, C = x.shape
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, Ho, Wo, C), dtype=torch.float32, device=x.device)
+    check(lib().edgedet_dwconv2d(_ptr(x), B, H, W, C, _ptr(w_taps), _ptr(bias), k, stride, pad, ACT[act], _ptr(y),
+                                 stream_handle()))
+    return y

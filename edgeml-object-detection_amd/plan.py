@@ -1,0 +1,238 @@
+"""Static execution plans: the host side of the engine.
+
+A detector forward for a fixed (batch, height, width) is lowered once into
+  * a packed weight blob (BatchNorm folded in float64, conv weights K-contiguous
+    [Cout][KH][KW][Cin] with K padded to 32, depthwise weights tap-major [K*K][C], SE fc weights
+    transposed), uploaded once per model and shared by every plan of that model;
+  * one device arena (a single torch allocation, 256-byte aligned carve-outs) holding every
+    activation, the NHWC input staging buffer and the output buffers;
+  * an array of edgedet_op records (numpy, layout = include/edgedet.h) that libedgedet.so runs
+    directly or captures into a hipGraph replayed per batch.
+Nothing here computes detections: every FLOP runs in the HIP kernels of libedgedet.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import ops
+
+ALIGN = 256
+
+
+# ------------------------------------------------------------------------------ weights
+class WeightPack:
+    """Host-side collection of float32 arrays packed into one device blob."""
+
+    def __init__(self):
+        self.arrays = []
+        self.size = 0  # in floats
+        self.device_blob = None
+
+    def add(self, arr):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32)).reshape(-1)
+        off = self.size
+        self.arrays.append((off, a))
+        self.size = off + ((a.size + 63) // 64) * 64
+        return WRef(self, off, a.size)
+
+    def upload(self, device):
+        if self.device_blob is not None and self.device_blob.device == torch.device(device):
+            return self.device_blob
+        host = np.zeros(self.size, dtype=np.float32)
+        for off, a in self.arrays:
+            host[off:off + a.size] = a
+        self.device_blob = torch.from_numpy(host).to(device)
+        return self.device_blob
+
+
+class WRef:
+    def __init__(self, pack, off, n):
+        self.pack, self.off, self.n = pack, off, n
+
+    def ptr(self):
+        return self.pack.device_blob.data_ptr() + 4 * self.off
+
+
+def fold_bn(w, gamma, beta, mean, var, eps):
+    """Eval BatchNorm folded into the preceding bias-free conv (float64 math, float32 result)."""
+    w = np.asarray(w, dtype=np.float64)
+    scale = np.asarray(gamma, np.float64) / np.sqrt(np.asarray(var, np.float64) + eps)
+    wf = w * scale.reshape((-1,) + (1,) * (w.ndim - 1))
+    bf = np.asarray(beta, np.float64) - np.asarray(mean, np.float64) * scale
+    return wf.astype(np.float32), bf.astype(np.float32)
+
+
+def pack_conv_weight(w_oihw, cin_pad=None):
+    """[Cout][Cin][KH][KW] -> [Cout][Kpad] with K = KH*KW*Cin ordered (kh, kw, ci), zero padded."""
+    w = np.asarray(w_oihw, dtype=np.float32)
+    cout, cin, kh, kw = w.shape
+    if cin_pad and cin_pad > cin:
+        w = np.concatenate([w, np.zeros((cout, cin_pad - cin, kh, kw), np.float32)], axis=1)
+        cin = cin_pad
+    k = kh * kw * cin
+    kpad = (k + 31) // 32 * 32
+    out = np.zeros((cout, kpad), dtype=np.float32)
+    out[:, :k] = w.transpose(0, 2, 3, 1).reshape(cout, k)
+    return out, k, kpad, cin
+
+
+def pack_dw_weight(w_c1kk):
+    w = np.asarray(w_c1kk, dtype=np.float32)
+    c, _, kh, kw = w.shape
+    return w.reshape(c, kh * kw).T.copy()
+
+
+# ------------------------------------------------------------------------------ arena + ops
+class Buf:
+    """A carve-out of the plan arena (float32 unless dtype says otherwise)."""
+
+    def __init__(self, shape, dtype=torch.float32, name=""):
+        self.shape = tuple(int(s) for s in shape)
+        self.dtype = dtype
+        self.name = name
+        self.nbytes = int(np.prod(self.shape)) * torch.tensor([], dtype=dtype).element_size()
+        self.off = None
+        self.plan = None
+
+    def ptr(self):
+        return self.plan.arena.data_ptr() + self.off
+
+    def tensor(self):
+        n = int(np.prod(self.shape))
+        es = torch.tensor([], dtype=self.dtype).element_size()
+        flat = self.plan.arena[self.off:self.off + n * es].view(self.dtype)
+        return flat.view(self.shape)
+
+
+class Op:
+    def __init__(self, kind, i=None, p=None, f=None, d=None, name=""):
+        self.kind, self.name = kind, name
+        self.i = dict(i or {})
+        self.p = dict(p or {})
+        self.f = dict(f or {})
+        self.d = dict(d or {})
+
+
+class Plan:
+    """A lowered forward: ops + arena + weights; run() or run via a captured hipGraph."""
+
+    def __init__(self, weights, device):
+        self.weights = weights
+        self.device = torch.device(device)
+        self.ops = []
+        self.bufs = []
+        self.arena = None
+        self.records = None
+        self.graph = None
+        self.consts = []  # host arrays uploaded into the arena at finalize (anchors, ratios)
+
+    # building -----------------------------------------------------------------------------
+    def buf(self, shape, dtype=torch.float32, name=""):
+        b = Buf(shape, dtype, name)
+        b.plan = self
+        self.bufs.append(b)
+        return b
+
+    def const(self, arr, dtype=torch.float32, name=""):
+        a = np.ascontiguousarray(arr)
+        b = self.buf(a.shape, dtype, name)
+        self.consts.append((b, a))
+        return b
+
+    def add(self, op):
+        self.ops.append(op)
+        return op
+
+    # finalizing ---------------------------------------------------------------------------
+    def finalize(self):
+        off = 0
+        for b in self.bufs:
+            b.off = off
+            off += (b.nbytes + ALIGN - 1) // ALIGN * ALIGN
+        self.arena = torch.zeros(max(off, ALIGN), dtype=torch.uint8, device=self.device)
+        self.weights.upload(self.device)
+        for b, a in self.consts:
+            b.tensor().copy_(torch.from_numpy(a).to(b.dtype))
+        rec = np.zeros(len(self.ops), dtype=ops.OP_DTYPE)
+        for k, op in enumerate(self.ops):
+            rec[k]["kind"] = op.kind
+            for j, v in op.i.items():
+                rec[k]["i"][j] = int(v)
+            for j, v in op.p.items():
+                if v is None:
+                    rec[k]["p"][j] = 0
+                elif isinstance(v, (Buf, WRef)):
+                    rec[k]["p"][j] = v.ptr()
+                else:
+                    rec[k]["p"][j] = int(v)
+            for j, v in op.f.items():
+                rec[k]["f"][j] = float(v)
+            for j, v in op.d.items():
+                rec[k]["d"][j] = float(v)
+        self.records = rec
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return self
+
+    @property
+    def arena_bytes(self):
+        return 0 if self.arena is None else self.arena.numel()
+
+    # running ------------------------------------------------------------------------------
+    def run(self, stream=None):
+        L = ops.lib()
+        ops.check(L.edgedet_plan_run(self.records.ctypes.data_as(ctypes.c_void_p), len(self.records),
+                                     ops.stream_handle(stream)))
+
+    def capture(self, stream):
+        """Capture the plan into a hipGraph on `stream` (a non-default torch.cuda.Stream)."""
+        L = ops.lib()
+        if self.graph is not None:
+            L.edgedet_graph_destroy(self.graph)
+            self.graph = None
+        # warm the kernels' one-time attribute setup outside of capture
+        with torch.cuda.stream(stream):
+            self.run(stream)
+        stream.synchronize()
+        g = ctypes.c_void_p()
+        ops.check(L.edgedet_graph_create(self.records.ctypes.data_as(ctypes.c_void_p), len(self.records),
+                                         ops.stream_handle(stream), ctypes.byref(g)))
+        self.graph = g
+        return self
+
+    def replay(self, stream):
+        ops.check(ops.lib().edgedet_graph_launch(self.graph, ops.stream_handle(stream)))
+
+    def __del__(self):
+        try:
+            if self.graph is not None and ops._LIB is not None:
+                ops._LIB.edgedet_graph_destroy(self.graph)
+        except Exception:
+            pass
+
+    def summary(self):
+        kinds = {}
+        for op in self.ops:
+            kinds[op.kind] = kinds.get(op.kind, 0) + 1
+        return {"ops": len(self.ops), "by_kind": kinds, "arena_MB": self.arena_bytes / 2 ** 20,
+                "weights_MB": self.weights.size * 4 / 2 ** 20}
+
+
+# ------------------------------------------------------------------------------ op helpers
+def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K, Kpad, res=None, res_hw=None,
+            in_scale=None, y_pstride=None, y_bstride=None, y_off=0, x_pstride=None, x_bstride=None, tile=0,
+            name=""):
+    """Build a CONV record.  x_shape = (B, H, W, C) as laid out in x; y_shape = (B, Ho, Wo, Cout)."""
+    B, H, W, C = x_shape
+    _, Ho, Wo, _ = y_shape
+    assert Ho == (H + 2 * pad - k) // stride + 1 and Wo == (W + 2 * pad - k) // stride + 1, name
+    assert K == k * k * C, (name, K, k, C)
+    xp = C if x_pstride is None else x_pstride
+    yp = cout if y_pstride is None else y_pstride
+    rH, rW = res_hw if res_hw is not None else (Ho, Wo)
+    i = {0: B, 1: H, 2: W, 3: C, 4: Ho, 5: Wo, 6: cout, 7: k, 8: k, 9: stride, 10: pad, 11: ops.ACT[act], 12: K,
+         13: Kpad, 14: xp, 15: yp, 16: cout, 17: (H * W * xp if x_bstride is None else x_bstride),
+         18: (Ho * Wo * yp if y_bstride is None else y_bstride), 19: rH * rW * cout, 20: y_off, 21: rH, 22: rW,
+         23: tile}
+    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale}, name=name))

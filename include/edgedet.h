@@ -1,0 +1,127 @@
+/*
+ * edgedet.h — C-ABI of libedgedet.so, the MI355X (gfx950) detection-output engine.
+ *
+ * This library is the native half of the drop-in replacement for the hot path of
+ * torch_models/detect.py (the torchvision forward called at detect.py:78 for the models built by
+ * load_weak_models, detect.py:15-42).  The reference has no FFI of its own (no native
+ * code); its operator boundary is the torchvision detection-model call
+ *     model(Tensor[N,3,H,W] float32 in [0,1]) -> List[{"boxes","scores","labels"}]   (detect.py:78-81)
+ * and the torchvision C++ operators that call reaches (torchvision::nms, torchvision::roi_align and the
+ * ATen convolutions).  Each entry point below names the reference operator it replaces.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer unless its name starts with `host_`;
+ *   - the caller owns every buffer (images, packed weights, workspace, outputs); nothing here
+ *     allocates on the hot path;
+ *   - every call is asynchronous on the given stream (hipStream_t passed as void*; NULL = default);
+ *   - return value: 0 = ok, < 0 = error; edgedet_last_error() returns the message (thread-local).
+ *   - activations are NHWC float32; boxes are (x1, y1, x2, y2) float32.
+ */
+#ifndef EDGEDET_H
+#define EDGEDET_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------- plan ops */
+/*
+ * One step of a static execution plan.  The Python host (edgeml_amd/plan.py) lowers a detector
+ * into an array of these (BatchNorm folded, weights packed, buffers carved from one arena) and the
+ * native executor launches them in order.  Field meaning per `kind` is documented in plan.py and
+ * csrc/exec.cpp; sizes and pointers are plain integers so the layout is identical from ctypes.
+ */
+#define EDGEDET_OP_INTS 48
+#define EDGEDET_OP_PTRS 24
+#define EDGEDET_OP_DBLS 8
+#define EDGEDET_OP_FLTS 16
+
+typedef struct edgedet_op {
+    int64_t kind;
+    int64_t i[EDGEDET_OP_INTS];
+    uint64_t p[EDGEDET_OP_PTRS];
+    double d[EDGEDET_OP_DBLS]; /* thresholds compared in double, as the reference's CPU nms */
+    float f[EDGEDET_OP_FLTS];
+} edgedet_op;
+
+enum {
+    EDGEDET_OP_MEMSET = 1,        /* zero p[0] for i[0] bytes                                         */
+    EDGEDET_OP_PREPROCESS = 2,    /* GeneralizedRCNNTransform: normalize, bilinear resize, zero pad   */
+    EDGEDET_OP_CONV = 3,          /* conv2d + folded BN + bias + residual/upsample-add + activation   */
+    EDGEDET_OP_DWCONV = 4,        /* depthwise conv2d + folded BN + activation                        */
+    EDGEDET_OP_CHANNEL_MEAN = 5,  /* adaptive_avg_pool2d(1) (SqueezeExcitation squeeze)               */
+    EDGEDET_OP_SE_FC = 6,         /* SqueezeExcitation fc1-ReLU-fc2-Hardsigmoid                       */
+    EDGEDET_OP_MAXPOOL = 7,       /* max_pool2d (ResNet stem 3x3 s2 p1, FPN LastLevelMaxPool 1x1 s2)  */
+    EDGEDET_OP_SSD_SCORES = 8,    /* SSD softmax + BoxCoder.decode + clip                             */
+    EDGEDET_OP_SSD_CLASS_NMS = 9, /* per (image, class): score>t, top-k, NMS                          */
+    EDGEDET_OP_MERGE_TOPK = 10,   /* per image: merge kept lists, sort by score, keep[:N], rescale    */
+    EDGEDET_OP_RPN_LEVEL_NMS = 11,/* per (image, FPN level): top-k logits, decode, clip, small, NMS   */
+    EDGEDET_OP_ROI_ALIGN = 12,    /* MultiScaleRoIAlign (LevelMapper + roi_align 7x7, sr=2)          */
+    EDGEDET_OP_BOX_SCORES = 13,   /* RoIHeads softmax + class-specific decode + clip                 */
+    EDGEDET_OP_BOX_CLASS_NMS = 14 /* per (image, class): score>t, remove_small, NMS                   */
+};
+
+/* Run ops[0..n) on `stream`.  Shapes are checked on the host before any launch. */
+int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream);
+
+/* Capture ops[0..n) into a hipGraph (instantiated); *graph receives an opaque handle. */
+int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** graph);
+int edgedet_graph_launch(void* graph, void* stream);
+int edgedet_graph_destroy(void* graph);
+
+/* ------------------------------------------------------------------------ unit operators */
+/*
+ * torchvision::nms (reference call sites: SSD postprocess, RPN filter_proposals and RoIHeads
+ * postprocess_detections, all reached from detect.py:78; semantics SURVEY.md App. A.0).
+ * boxes [n,4], scores [n] -> keep [n] int64 (indices, score-descending, ties lower index first),
+ * *d_num_keep int32.  n <= 1024.  Suppress j when inter/(area_i+area_j-inter) > iou_threshold.
+ */
+int edgedet_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
+                int64_t* keep, int32_t* d_num_keep, void* stream);
+
+/*
+ * torchvision::ops.batched_nms (per-group greedy NMS; result sorted by score descending, ties by
+ * lower index).  Equivalent to the reference's _batched_nms_vanilla.  n <= 1024.
+ */
+int edgedet_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, int64_t n,
+                        double iou_threshold, int64_t* keep, int32_t* d_num_keep, void* stream);
+
+/*
+ * torchvision::roi_align forward, aligned=False (MultiScaleRoIAlign's call),
+ * on an NHWC feature map.  feat [B,H,W,C]; rois [R,5] (batch_idx, x1, y1, x2, y2);
+ * out [R,PH,PW,C] (NHWC; the reference's NCHW output permuted).
+ */
+int edgedet_roi_align(const float* feat, int64_t B, int64_t H, int64_t W, int64_t C,
+                      const float* rois, int64_t R, float spatial_scale, int32_t pooled_h,
+                      int32_t pooled_w, int32_t sampling_ratio, float* out, void* stream);
+
+/*
+ * ATen conv2d (+ eval BatchNorm folded into w/bias, + activation), the layers of the torchvision
+ * backbones/heads reached from detect.py:78.  x NHWC [B,H,W,Cin]; w [Cout][KH][KW][Cin] (packed:
+ * K = KH*KW*Cin padded to a multiple of 32 with zeros, see edgedet_conv_weight_k); bias [Cout];
+ * res (nullable) NHWC [B,Ho,Wo,Cout] added before the activation; y NHWC [B,Ho,Wo,Cout].
+ * act: 0 none, 1 relu, 2 relu6, 3 hardswish, 4 hardsigmoid, 5 sigmoid.
+ */
+int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                   const float* bias, int64_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                   int32_t pad, int32_t act, const float* res, float* y, void* stream);
+int64_t edgedet_conv_weight_k(int32_t KH, int32_t KW, int64_t Cin);
+
+/* Depthwise conv2d (+ folded BN + act).  x NHWC [B,H,W,C]; w [KH*KW][C]; bias [C]. */
+int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,
+                     const float* bias, int32_t K, int32_t stride, int32_t pad, int32_t act,
+                     float* y, void* stream);
+
+/* --------------------------------------------------------------------------------- misc */
+const char* edgedet_last_error(void);
+/* Library/ABI version: (major << 16) | minor. */
+int32_t edgedet_version(void);
+/* Device code target the library was built for ("gfx950"). */
+const char* edgedet_target(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDGEDET_H */

@@ -102,6 +102,9 @@ def make_g1():
                 p["labels"] = np.arange(91, dtype=np.int64)
             preds.append(p)
             sizes[name] = (h, w)
+        # detect.py:92 decrements the label array in place (`labels -= 1` on a numpy view of the
+        # model's tensor), so keep pristine copies of the inputs for the fixture
+        orig = {name[:-4]: {k: v.copy() for k, v in p.items()} for (_, name, h, w, n), p in zip(items, preds)}
         install_stub(preds, sizes)
         for m in list(sys.modules):
             if m in ("detect", "coco_labelmap"):
@@ -121,9 +124,9 @@ def make_g1():
                 key = name[:-4]
                 with open(os.path.join(save_dir, key + ".npy"), "rb") as f:
                     raw = f.read()
-                out[f"{ds}/{key}/boxes"] = p["boxes"]
-                out[f"{ds}/{key}/scores"] = p["scores"]
-                out[f"{ds}/{key}/labels"] = p["labels"]
+                out[f"{ds}/{key}/boxes"] = orig[key]["boxes"]
+                out[f"{ds}/{key}/scores"] = orig[key]["scores"]
+                out[f"{ds}/{key}/labels"] = orig[key]["labels"]
                 out[f"{ds}/{key}/hw"] = np.array([h, w], dtype=np.int64)
                 out[f"{ds}/{key}/npy_bytes"] = np.frombuffer(raw, dtype=np.uint8)
     import coco_labelmap

@@ -1,0 +1,63 @@
+"""World-size-2 gloo tests of the sharding and the output-row gather."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rows_for(name):
+    rs = np.random.RandomState(int(name) % 97)
+    n = int(name) % 4  # includes empty (0,6) outputs
+    return rs.rand(n, 6)
+
+
+def _worker(rank, world, port, names, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from edgeml_amd import distributed as D
+    mine = D.shard(names, rank, world)
+    res = {n: _rows_for(n) for n in mine}
+    out = D.gather_rows(res, mine, names, rank, world)
+    if rank == 0:
+        q.put({k: v.tolist() for k, v in out.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_is_contiguous_partition():
+    from edgeml_amd import distributed as D
+    names = [f"{i:012d}.jpg" for i in range(103)]
+    for world in (1, 2, 3, 8):
+        parts = [D.shard(names, r, world) for r in range(world)]
+        assert sum(parts, []) == names
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+@pytest.mark.parametrize("n", [7, 1])
+def test_gather_rows_world2(n):
+    names = [f"{i:06d}" for i in range(n)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(got) == names
+    for k in names:
+        np.testing.assert_array_equal(np.asarray(got[k]).reshape(-1, 6), _rows_for(k))

@@ -1,0 +1,116 @@
+"""GPU unit parity: each libedgedet kernel against an fp32 CPU reference of the same op.
+
+Conv / depthwise: torch fp32 CPU conv2d (NCHW) of the same folded weights (float tolerance).
+RoIAlign / NMS: the oracle's C restatement of torchvision's CPU kernels (oracle/c/tvops_ref.c);
+NMS indices must match exactly, RoIAlign values bit-for-bit (same op order, no contraction).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _act(y, act):
+    return {None: y, "RE": F.relu(y), "R6": F.relu6(y), "HS": F.hardswish(y)}[act]
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,act,res", [
+    (2, 17, 19, 4, 16, 3, 2, "HS", False),      # SSD stem shape class (Cin padded to 4)
+    (2, 20, 20, 112, 672, 1, 1, "HS", False),   # expansion 1x1
+    (3, 10, 10, 480, 80, 1, 1, None, True),     # projection with residual
+    (1, 25, 23, 64, 64, 3, 1, "RE", False),     # ResNet 3x3
+    (1, 26, 26, 128, 256, 3, 2, "RE", True),    # strided 3x3 + residual
+    (1, 40, 36, 4, 64, 7, 2, "RE", False),      # ResNet stem 7x7 (Cin padded to 4)
+    (2, 7, 7, 256, 24, 1, 1, None, False),      # narrow Cout
+    (4, 1, 1, 1024, 455, 1, 1, None, False),    # FC as 1x1 (predictor shape)
+])
+def test_conv_matches_torch(B, H, W, Cin, Cout, k, s, act, res):
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    pad = (k - 1) // 2
+    ref = F.conv2d(x, w, b, s, pad)
+    r = torch.randn_like(ref) if res else None
+    if res:
+        ref = ref + r
+    ref = _act(ref, act)
+    wp, K, Kpad, _ = pack_conv_weight(w.numpy())
+    out = ops.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(wp).to(DEV), b.to(DEV), Cout,
+                          k, s, pad, act, r.permute(0, 2, 3, 1).contiguous().to(DEV) if res else None)
+    got = out.permute(0, 3, 1, 2).cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("B,H,W,C,k,s,act", [(2, 20, 20, 72, 5, 2, "RE"), (3, 10, 10, 672, 5, 1, "HS"),
+                                              (2, 3, 3, 128, 3, 2, "R6"), (1, 40, 40, 64, 3, 1, "RE")])
+def test_dwconv_matches_torch(B, H, W, C, k, s, act):
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_dw_weight
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(C, 1, k, k, generator=g) / k
+    b = torch.randn(C, generator=g) * 0.1
+    ref = _act(F.conv2d(x, w, b, s, (k - 1) // 2, 1, C), act)
+    out = ops.dwconv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(pack_dw_weight(w.numpy())).to(DEV),
+                            b.to(DEV), k, s, (k - 1) // 2, act)
+    err = (out.permute(0, 3, 1, 2).cpu() - ref).abs().max().item()
+    assert err < 1e-5, err
+
+
+def _rand_boxes(rs, n, scale=100.0):
+    xy = rs.uniform(0, scale, (n, 2)).astype(np.float32)
+    wh = rs.uniform(1, scale / 3, (n, 2)).astype(np.float32)
+    return np.concatenate([xy, xy + wh], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("n,thr,seed", [(0, 0.5, 0), (1, 0.5, 0), (37, 0.5, 1), (300, 0.55, 2), (1000, 0.7, 3),
+                                        (1024, 0.3, 4)])
+def test_nms_matches_oracle(n, thr, seed):
+    from edgeml_amd import ops
+    from oracle import tv_ops
+    rs = np.random.RandomState(seed)
+    boxes = _rand_boxes(rs, n)
+    scores = rs.uniform(0, 1, n).astype(np.float32)
+    if n > 10:
+        scores[5:10] = scores[0]  # ties
+    ref = tv_ops.nms(boxes, scores, thr) if n else np.zeros(0, np.int64)
+    got = ops.nms(torch.from_numpy(boxes).to(DEV), torch.from_numpy(scores).to(DEV), thr).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_batched_nms_matches_oracle():
+    from edgeml_amd import ops
+    from oracle import tv_ops
+    rs = np.random.RandomState(5)
+    n = 800
+    boxes = _rand_boxes(rs, n, 60.0)
+    scores = rs.uniform(0, 1, n).astype(np.float32)
+    idxs = rs.randint(0, 7, n).astype(np.int64)
+    ref = tv_ops.batched_nms(boxes, scores, idxs, 0.5)
+    got = ops.batched_nms(torch.from_numpy(boxes).to(DEV), torch.from_numpy(scores).to(DEV),
+                          torch.from_numpy(idxs).to(DEV), 0.5).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_roi_align_matches_oracle():
+    from edgeml_amd import ops
+    from oracle import tv_ops
+    rs = np.random.RandomState(6)
+    B, C, H, W = 2, 32, 25, 31
+    feat = torch.from_numpy(rs.randn(B, C, H, W).astype(np.float32))
+    R = 64
+    bx = _rand_boxes(rs, R, 120.0)
+    bx[:4] = [[-10, -10, 5, 5], [0, 0, 1, 1], [100, 90, 130, 140], [50, 50, 50.5, 50.2]]
+    rois = np.concatenate([rs.randint(0, B, (R, 1)).astype(np.float32), bx], 1).astype(np.float32)
+    ref = tv_ops.roi_align(feat, rois, 0.25)
+    got = ops.roi_align_nhwc(feat.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(rois).to(DEV), 0.25)
+    got = got.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(got, ref), (got - ref).abs().max().item()

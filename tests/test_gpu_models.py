@@ -1,0 +1,78 @@
+"""GPU parity of the full detectors against the CPU oracle (oracle/ssdlite.py, oracle/frcnn.py).
+
+Raw head outputs must agree to fp32 tolerance; final detections (after the discrete score
+threshold / top-k / NMS decisions) must agree row by row within 1e-3 (north_star tolerance).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.parity import compare_detections, set_match
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ssd():
+    from edgeml_amd import models, synthetic
+    sd = synthetic.synthetic_state_dict("ssd", 91, True, seed=0)
+    return sd, models.SSDLite320(sd, 91, True).to("cuda")
+
+
+@pytest.fixture(scope="module")
+def frcnn():
+    from edgeml_amd import models, synthetic
+    sd = synthetic.synthetic_state_dict("faster_rcnn", 91, seed=0)
+    return sd, models.FasterRCNNFPNv2(sd, 91).to("cuda")
+
+
+def test_ssd_raw_heads_match_oracle(ssd):
+    from edgeml_amd import synthetic
+    from oracle.ssdlite import SSDLiteOracle
+    sd, model = ssd
+    imgs = synthetic.make_batch(2, 640, 640, seed=11)
+    o = SSDLiteOracle(sd, 91, True)
+    cls_ref, reg_ref, _ = o.forward_raw(list(imgs))
+    plan = model.plan(2, 640, 640)
+    plan.input.tensor().copy_(imgs.cuda())
+    plan.run()
+    torch.cuda.synchronize()
+    cls = plan.cls_logits.tensor().cpu()
+    reg = plan.bbox_regression.tensor().cpu()
+    ec = (cls - cls_ref).abs().max().item()
+    er = (reg - reg_ref).abs().max().item()
+    print(f"ssd raw: max|dcls|={ec:.3e} (ref max {cls_ref.abs().max():.2f}) max|dreg|={er:.3e}")
+    assert ec < 2e-3 and er < 2e-3
+
+
+@pytest.mark.parametrize("h,w,n", [(640, 640, 2), (480, 640, 1)])
+def test_ssd_detections_match_oracle(ssd, h, w, n):
+    from edgeml_amd import synthetic
+    from oracle.ssdlite import SSDLiteOracle
+    sd, model = ssd
+    imgs = synthetic.make_batch(n, h, w, seed=21 + h)
+    ref = SSDLiteOracle(sd, 91, True)(list(imgs))
+    got = model(imgs.cuda())
+    for r, g in zip(ref, got):
+        rep = compare_detections(r, g)
+        frac = set_match(r, g)
+        print("ssd", h, w, rep, "set-match", frac)
+        assert rep["n_ref"] > 0
+        assert frac >= 0.99 and abs(rep["n_ref"] - rep["n_got"]) <= 2
+
+
+def test_frcnn_detections_match_oracle(frcnn):
+    from edgeml_amd import synthetic
+    from oracle.frcnn import FasterRCNNOracle
+    sd, model = frcnn
+    imgs = synthetic.make_batch(1, 640, 640, seed=31)
+    o = FasterRCNNOracle(sd, 91)
+    ref = o(list(imgs))
+    got = model(imgs.cuda())
+    plan = model.plan(1, 640, 640)
+    print("frcnn proposals", plan.proposal_count.tensor().cpu().tolist())
+    for r, g in zip(ref, got):
+        rep = compare_detections(r, g)
+        frac = set_match(r, g)
+        print("frcnn", rep, "set-match", frac)
+        assert frac >= 0.98

@@ -1,0 +1,167 @@
+"""CPU tests of the host side: architecture tables, anchors, plan lowering, the C-ABI library."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_param_counts_match_published():
+    """SURVEY.md §6 known answers (torchvision model cards)."""
+    from edgeml_amd import arch
+    assert arch.param_count(arch.ssdlite_table(91, True)) == 3_440_060
+    assert arch.param_count(arch.ssdlite_table(91, False)) == 5_198_540
+    assert arch.param_count(arch.frcnn_table(91)) == 43_712_278
+
+
+def test_ssd_anchors_match_oracle():
+    from edgeml_amd import anchors
+    from oracle import tv_ops
+    grids = [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
+    a = anchors.ssd_default_boxes(grids)
+    b = tv_ops.ssd_default_boxes(grids).numpy()
+    assert a.shape == (3234, 4)
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("hp,wp", [(800, 800), (608, 800), (800, 1088)])
+def test_rpn_anchors_match_oracle(hp, wp):
+    from edgeml_amd import anchors
+    from oracle import tv_ops
+    grids = [(hp // 4, wp // 4), (hp // 8, wp // 8), (hp // 16, wp // 16), (hp // 32, wp // 32),
+             ((hp // 32 + 1) // 2, (wp // 32 + 1) // 2)]
+    for x, y in zip(anchors.rpn_anchors(grids, (hp, wp)), tv_ops.rpn_anchors(grids, (hp, wp))):
+        np.testing.assert_array_equal(x, y.numpy())
+    if (hp, wp) == (800, 800):
+        assert sum(len(x) for x in anchors.rpn_anchors(grids, (hp, wp))) == 159_882
+
+
+def test_fold_bn_matches_conv_then_bn():
+    import torch.nn.functional as F
+    from edgeml_amd.plan import fold_bn
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 8, 9, 9, generator=g)
+    w = torch.randn(16, 8, 3, 3, generator=g)
+    gam, bet = torch.rand(16, generator=g) + 0.5, torch.randn(16, generator=g)
+    mu, var = torch.randn(16, generator=g), torch.rand(16, generator=g) + 0.1
+    ref = F.batch_norm(F.conv2d(x, w, None, 1, 1), mu, var, gam, bet, False, 0.0, 1e-3)
+    wf, bf = fold_bn(w.numpy(), gam.numpy(), bet.numpy(), mu.numpy(), var.numpy(), 1e-3)
+    got = F.conv2d(x, torch.from_numpy(wf), torch.from_numpy(bf), 1, 1)
+    assert (got - ref).abs().max() < 1e-4
+
+
+def test_pack_conv_weight_layout():
+    from edgeml_amd.plan import pack_conv_weight
+    w = np.arange(2 * 3 * 3 * 3, dtype=np.float32).reshape(2, 3, 3, 3)
+    p, K, Kpad, cin = pack_conv_weight(w, cin_pad=4)
+    assert (K, Kpad, cin) == (36, 64, 4)
+    # element (o, kh, kw, ci) at column (kh*3 + kw)*4 + ci
+    for o, ci, kh, kw in [(0, 0, 0, 0), (1, 2, 2, 1), (1, 1, 0, 2)]:
+        assert p[o, (kh * 3 + kw) * 4 + ci] == w[o, ci, kh, kw]
+    assert np.all(p[:, 3::4][:, :9] == 0) and np.all(p[:, 36:] == 0)
+
+
+def test_fastdiv_emulation():
+    """csrc/common.hpp FastDiv (multiply-high) for every divisor the kernels use."""
+    def make(d):
+        s = 0
+        while (1 << s) < d:
+            s += 1
+        m = ((1 << 32) * ((1 << s) - d)) // d + 1
+        return m & 0xffffffff, s
+
+    rs = np.random.RandomState(0)
+    for d in [1, 2, 3, 4, 7, 13, 24, 40, 49, 100, 112, 160, 400, 1600, 2500, 40000, 160000, 12544, 3234]:
+        m, s = make(d)
+        ns = np.concatenate([np.arange(0, 5000), rs.randint(0, 2 ** 31 - 1, 5000)]).astype(np.uint64)
+        q = ((((ns * np.uint64(m)) >> np.uint64(32)) + ns) >> np.uint64(s))
+        np.testing.assert_array_equal(q, ns // np.uint64(d))
+
+
+def _declared_symbols():
+    with open(os.path.join(ROOT, "include", "edgedet.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(edgedet_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from edgeml_amd import ops
+    lib = ops.lib()
+    declared = _declared_symbols()
+    assert set(declared) == set(ops.EXPORTS), declared
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.edgedet_target() == b"gfx950"
+    assert lib.edgedet_version() >= (1 << 16)
+    assert lib.edgedet_conv_weight_k(3, 3, 4) == 64
+
+
+def test_op_record_layout_matches_header():
+    from edgeml_amd import ops
+    with open(os.path.join(ROOT, "include", "edgedet.h")) as f:
+        txt = f.read()
+    ints = int(re.search(r"#define EDGEDET_OP_INTS (\d+)", txt).group(1))
+    ptrs = int(re.search(r"#define EDGEDET_OP_PTRS (\d+)", txt).group(1))
+    dbls = int(re.search(r"#define EDGEDET_OP_DBLS (\d+)", txt).group(1))
+    flts = int(re.search(r"#define EDGEDET_OP_FLTS (\d+)", txt).group(1))
+    assert (ints, ptrs, dbls, flts) == (ops.OP_INTS, ops.OP_PTRS, ops.OP_DBLS, ops.OP_FLTS)
+    kinds = dict(re.findall(r"EDGEDET_OP_([A-Z_]+) = (\d+)", txt))
+    for k, v in kinds.items():
+        assert getattr(ops, k) == int(v), k
+
+
+def test_unit_ops_refuse_cpu_tensors():
+    from edgeml_amd import ops
+    with pytest.raises(ValueError):
+        ops.nms(torch.zeros(3, 4), torch.zeros(3), 0.5)
+
+
+def test_models_refuse_cpu_device():
+    from edgeml_amd import models
+    m = models.ssdlite320_mobilenet_v3_large()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.to("cpu")
+
+
+def test_state_dict_validation():
+    from edgeml_amd import models, synthetic
+    sd = synthetic.synthetic_state_dict("ssd", 91, True)
+    sd.pop("head.regression_head.module_list.0.1.bias")
+    with pytest.raises(RuntimeError, match="missing keys"):
+        models.SSDLite320(sd, 91, True)
+
+
+def test_ssd_plan_lowering():
+    """The op list covers every layer and the arena/offset bookkeeping is consistent."""
+    from edgeml_amd import models, ops
+    m = models.ssdlite320_mobilenet_v3_large()
+    P = m.build_plan(4, 640, 480)
+    kinds = [op.kind for op in P.ops]
+    assert kinds[0] == ops.PREPROCESS and kinds[-1] == ops.MERGE_TOPK
+    # convs: stem 1 + blocks 0-11 (block 0 has no expansion: 1 + 11*2) + C4 split 2 + blocks 13-14 (2*2)
+    #        + last 1 + extras 4*2 + head 6*2
+    n_conv = kinds.count(ops.CONV)
+    n_dw = kinds.count(ops.DWCONV)
+    assert n_dw == 15 + 4 + 12
+    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12
+    assert kinds.count(ops.SE_FC) == 8
+    assert m.grids == [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
+    for op in P.ops:
+        if op.kind == ops.CONV:
+            assert op.i[12] == op.i[7] * op.i[8] * op.i[3] and op.i[13] % 32 == 0
+
+
+def test_frcnn_plan_lowering():
+    from edgeml_amd import models, ops
+    m = models.fasterrcnn_resnet50_fpn_v2()
+    P = m.build_plan(2, 480, 640)
+    assert m.resized_size(480, 640) == (800, 1066)
+    pre = P.ops[0]
+    assert pre.i[5] == 800 and pre.i[6] == 1088  # padded to /32
+    kinds = [op.kind for op in P.ops]
+    assert kinds.count(ops.ROI_ALIGN) == 1 and kinds.count(ops.RPN_LEVEL_NMS) == 1
+    assert kinds.count(ops.CONV) == 1 + 16 * 3 + 4 + 8 + 5 * 3 + 4 + 2
