@@ -67,22 +67,60 @@ def timed_steps(plan, stream, steps, warmup, dist):
 
 
 # ------------------------------------------------------------------------------ per-op costs
+def conv_grid(op):
+    """(workgroups, threads per workgroup) of a CONV op, as csrc/conv.hip picks its tile."""
+    i = op.i
+    M, Cout = i[0] * i[4] * i[5], i[6]
+    tile = i[23] or (1 if Cout <= 32 else (2 if Cout <= 64 else 3))
+    bm, bn, nt = {1: (128, 32, 256), 2: (128, 64, 256), 3: (128, 128, 256), 4: (256, 128, 512)}[tile]
+    return -(-M // bm) * -(-Cout // bn), nt
+
+
 def op_work(op):
-    """(kind, algorithmic flops, algorithmic HBM bytes) of one plan op (None if not modelled)."""
+    """(family, algorithmic flops, algorithmic HBM bytes) of one plan op: every input read once,
+    every output written once (SURVEY.md §8d byte model)."""
     from edgeml_amd import ops as O
     i = op.i
-    if op.kind == O.CONV:
-        B, H, W, Cin, Ho, Wo, Cout, KH, KW = (i[k] for k in range(9))
+    k = op.kind
+    if k == O.CONV:
+        B, H, W, Cin, Ho, Wo, Cout, KH, KW = (i[j] for j in range(9))
         M = B * Ho * Wo
         flops = 2.0 * M * Cout * KH * KW * Cin
         byts = 4.0 * (B * H * W * Cin + Cout * KH * KW * Cin + M * Cout)
         if op.p.get(4) is not None:
             byts += 4.0 * M * Cout
         return "conv", flops, byts
-    if op.kind == O.DWCONV:
-        B, H, W, C, Ho, Wo, K = (i[k] for k in range(7))
+    if k == O.DWCONV:
+        B, H, W, C, Ho, Wo, K = (i[j] for j in range(7))
         return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
-    return None
+    if k == O.PREPROCESS:
+        B, H, W, Ho, Wo, Hp, Wp = (i[j] for j in range(7))
+        return "preprocess", 0.0, 4.0 * (B * 3 * H * W + B * Hp * Wp * 4)
+    if k == O.CHANNEL_MEAN:
+        return "se_squeeze", float(i[0] * i[1] * i[2]), 4.0 * i[0] * i[1] * i[2]
+    if k == O.SE_FC:
+        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * 2 * i[1] * i[2]
+    if k == O.MAXPOOL:
+        B, H, W, C, Ho, Wo = (i[j] for j in range(6))
+        return "maxpool", 0.0, 4.0 * (B * H * W * C + B * Ho * Wo * C)
+    if k == O.SSD_SCORES:
+        B, A, NC = i[0], i[1], i[2]
+        return "ssd_scores", 0.0, 4.0 * (2 * B * A * NC + 2 * B * A * 4 + A * 4)
+    if k == O.SSD_CLASS_NMS:
+        B, A, NC = i[0], i[1], i[2]
+        return "class_nms", 0.0, 4.0 * (B * NC * A + B * A * 4)
+    if k == O.MERGE_TOPK:
+        return "merge_topk", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
+    if k == O.RPN_LEVEL_NMS:
+        n = sum(i[6 + l] for l in range(i[1]))
+        return "rpn_nms", 0.0, 4.0 * i[0] * n * 5
+    if k == O.ROI_ALIGN:
+        return "roi_align", 0.0, 4.0 * 2 * i[1] * i[5] * i[6] * i[4]
+    if k == O.BOX_SCORES:
+        return "box_scores", 0.0, 4.0 * i[1] * i[2] * (i[0] + 5 * i[3])
+    if k == O.BOX_CLASS_NMS:
+        return "class_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 5
+    return f"kind{k}", 0.0, 0.0
 
 
 def per_op_times(plan, stream, reps=20):
@@ -109,35 +147,51 @@ def per_op_times(plan, stream, reps=20):
 
 
 def roofline_for(plan, stream, step_ms):
-    """Pick the kernel family that dominates the step and price its largest launch."""
+    """Dominant kernel family of the step (by measured device time) and its longest launch, priced
+    against the roof that binds it (max of flops / fp32-MFMA peak and bytes / HBM peak)."""
     times = per_op_times(plan, stream)
     fam = {}
     for op, t in zip(plan.ops, times):
-        w = op_work(op)
-        name = w[0] if w else f"kind{op.kind}"
+        name = op_work(op)[0]
         fam[name] = fam.get(name, 0.0) + t
     dom = max(fam, key=fam.get)
-    best = None
-    for op, t in zip(plan.ops, times):
-        w = op_work(op)
-        if w and w[0] == dom and (best is None or t > best[1]):
-            best = (op, t, w)
-    breakdown = {k: round(v, 4) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])}
-    if best is None:
-        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": dom, "family_ms": breakdown}
-    op, t, (name, flops, byts) = best
+    op, t = max(((o, t) for o, t in zip(plan.ops, times) if op_work(o)[0] == dom), key=lambda x: x[1])
+    name, flops, byts = op_work(op)
+    t_f = flops / (FP32_MFMA_PEAK_TFS * 1e12)
+    t_b = byts / (HBM_PEAK_GBS * 1e9)
+    out = {"kernel": {"conv": "conv_mfma_kernel", "dwconv": "dwconv_kernel"}.get(name, name), "launch": op.name,
+           "launch_ms": round(t, 4), "algorithmic_flops": flops, "algorithmic_bytes": byts,
+           "family_ms": {k: round(v, 4) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
+           "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
     if name == "conv":
+        out["grid_wg"], out["wg_threads"] = conv_grid(op)
+    if t_f >= t_b:
         ach = flops / (t * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFS, 4), "traffic": None, "kernel": "conv_mfma_kernel",
-                "launch": op.name, "launch_ms": round(t, 4), "algorithmic_flops": flops,
-                "family_ms": breakdown, "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
-    ach = byts / (t * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": name, "launch": op.name,
-            "launch_ms": round(t, 4), "algorithmic_bytes": byts, "family_ms": breakdown,
-            "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
+        out.update({"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(ach / FP32_MFMA_PEAK_TFS, 4)})
+    else:
+        ach = byts / (t * 1e-3) / 1e9
+        out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4)})
+    out["traffic"] = None
+    out["_op_index"] = plan.ops.index(op)
+    return out
+
+
+def attach_traffic(roof, model):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_<model>.json, produced by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied there); None if absent or stale."""
+    roof.pop("_op_index", None)
+    path = os.path.join(ROOT, "profiles", f"pmc_{model}.json")
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return
+    if pmc.get("launch") == roof.get("launch") and pmc.get("grid_wg") == roof.get("grid_wg"):
+        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        roof["traffic_source"] = os.path.relpath(path, ROOT)
 
 
 # ------------------------------------------------------------------------------ CPU baseline
@@ -193,6 +247,7 @@ def main():
                       "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
         if rank == 0 and not args.no_roofline:
             out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps)
+            attach_traffic(out["ssd"]["roofline"], "ssd")
         del plan
         m.plans.clear()
     if args.model in ("frcnn", "both"):
@@ -210,6 +265,7 @@ def main():
                         "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2)}
         if rank == 0 and not args.no_roofline:
             out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps)
+            attach_traffic(out["frcnn"]["roofline"], "frcnn")
         del plan
     if rank != 0:
         if dist:

@@ -236,6 +236,7 @@ static int launch_cfg(const ConvParams& p, hipStream_t s) {
 
 // Host launcher shared by the plan executor and the unit C entry point.
 int conv_launch(ConvParams p, int tile, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "conv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.Cin % 4 == 0, "conv: Cin must be a multiple of 4 (pad channels)");
     EDGEDET_REQUIRE(p.x_pstride % 4 == 0, "conv: input pixel stride must be a multiple of 4");
     EDGEDET_REQUIRE(p.Kpad % BK == 0 && p.Kpad >= p.K, "conv: Kpad must be a multiple of 32 and >= K");

@@ -601,8 +601,11 @@ static int set_lds(K kernel, size_t bytes) {
     return 0;
 }
 
+static bool seg_ok(const SegOut& o) { return o.box && o.score && o.tb && o.label && o.count && o.kmax > 0; }
+
 int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,
                       int B, int A, int NC, float img_h, float img_w, hipStream_t s) {
+    EDGEDET_REQUIRE(logits && reg && anchors && scores_t && boxes, "ssd_scores: null pointer");
     const int64_t total = (int64_t)B * A;
     hipLaunchKernelGGL(ssd_scores_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, logits, reg, anchors,
                        scores_t, boxes, B, A, NC, img_h, img_w);
@@ -612,6 +615,7 @@ int ssd_scores_launch(const float* logits, const float* reg, const float* anchor
 
 int box_scores_launch(const float* pred, int ld, int cls_off, int delta_off, const float* props, const int* counts,
                       float* scores, float* boxes, int B, int R, int NC, float img_h, float img_w, hipStream_t s) {
+    EDGEDET_REQUIRE(pred && props && counts && scores && boxes, "box_scores: null pointer");
     EDGEDET_REQUIRE(ld >= 5 * NC && ld % 4 == 0 && delta_off % 4 == 0, "box_scores: bad predictor layout");
     const int64_t total = (int64_t)B * R;
     hipLaunchKernelGGL(box_scores_kernel, dim3((unsigned)cdiv(total, 4)), dim3(256), 0, s, pred, ld, cls_off,
@@ -622,6 +626,7 @@ int box_scores_launch(const float* pred, int ld, int cls_off, int delta_off, con
 
 int ssd_class_nms_launch(const float* scores_t, const float* boxes, int B, int A, int NC, float score_thresh,
                          int topk, double iou, SegOut out, hipStream_t s) {
+    EDGEDET_REQUIRE(scores_t && boxes && seg_ok(out), "ssd_class_nms: null pointer");
     EDGEDET_REQUIRE(topk <= 512 && out.kmax >= topk, "ssd_class_nms: topk must be <= 512 and <= kmax");
     constexpr int KC = 512, NT = 256;
     auto k = ssd_class_nms_kernel<NT, KC>;
@@ -635,6 +640,9 @@ int ssd_class_nms_launch(const float* scores_t, const float* boxes, int B, int A
 int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s) {
     EDGEDET_REQUIRE(P.topk <= 1024 && out.kmax >= P.topk, "rpn: topk must be <= 1024 and <= kmax");
     EDGEDET_REQUIRE(P.nlevels >= 1 && P.nlevels <= 5, "rpn: 1..5 levels");
+    EDGEDET_REQUIRE(seg_ok(out), "rpn: null output records");
+    for (int l = 0; l < P.nlevels; ++l)
+        EDGEDET_REQUIRE(P.lv[l].head && P.lv[l].anchors && P.lv[l].n > 0, "rpn: null/empty level");
     constexpr int KC = 1024, NT = 512;
     auto k = rpn_level_nms_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;
@@ -645,6 +653,7 @@ int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s) {
 
 int box_class_nms_launch(const float* scores, const float* boxes, const int* counts, int B, int R, int NC,
                          float score_thresh, float min_size, double iou, SegOut out, hipStream_t s) {
+    EDGEDET_REQUIRE(scores && boxes && counts && seg_ok(out), "box_class_nms: null pointer");
     EDGEDET_REQUIRE(R <= 1024 && out.kmax >= R, "box_class_nms: R must be <= 1024 and <= kmax");
     constexpr int KC = 1024, NT = 512;
     auto k = box_class_nms_kernel<NT, KC>;
@@ -656,7 +665,9 @@ int box_class_nms_launch(const float* scores, const float* boxes, const int* cou
 }
 
 int merge_topk_launch(const MergeParams& P, int B, hipStream_t s) {
-    EDGEDET_REQUIRE(P.N <= 1024, "merge_topk: N must be <= 1024");
+    EDGEDET_REQUIRE(P.box && P.score && P.tb && P.label && P.count && P.out_box && P.out_score && P.out_count,
+                    "merge_topk: null pointer");
+    EDGEDET_REQUIRE(P.N <= 1024 && P.N > 0 && P.S > 0 && P.kmax > 0, "merge_topk: bad sizes");
     constexpr int KC = 1024, NT = 512;
     auto k = merge_topk_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;
@@ -672,6 +683,7 @@ using namespace edgedet;
 extern "C" int edgedet_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, int64_t n,
                                    double iou_threshold, int64_t* keep, int32_t* d_num_keep, void* stream) {
     EDGEDET_REQUIRE(n >= 0 && n <= 1024, "batched_nms: n must be in [0, 1024]");
+    EDGEDET_REQUIRE(d_num_keep && (n == 0 || (boxes && scores && keep)), "batched_nms: null pointer");
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) {
         EDGEDET_CHECK_HIP(hipMemsetAsync(d_num_keep, 0, sizeof(int32_t), s));

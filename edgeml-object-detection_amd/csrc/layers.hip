@@ -51,6 +51,7 @@ __global__ void preprocess_kernel(PreParams p) {
 
 int preprocess_launch(const PreParams& p0, hipStream_t s) {
     PreParams p = p0;
+    EDGEDET_REQUIRE(p.x && p.y, "preprocess: null x/y");
     EDGEDET_REQUIRE(p.Hp >= p.Ho && p.Wp >= p.Wo && p.Ho > 0 && p.Wo > 0, "preprocess: bad sizes");
     p.sh = (float)p.H / (float)p.Ho;
     p.sw = (float)p.W / (float)p.Wo;
@@ -99,6 +100,7 @@ __global__ void dwconv_kernel(DwParams p) {
 }
 
 int dwconv_launch(const DwParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
     const int64_t total = (int64_t)p.B * p.Ho * p.Wo * (p.C / 4);
     hipLaunchKernelGGL(dwconv_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
@@ -124,6 +126,7 @@ __global__ void channel_mean_kernel(const float* __restrict__ x, float* __restri
 }
 
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s) {
+    EDGEDET_REQUIRE(x && out, "channel_mean: null pointer");
     hipLaunchKernelGGL(channel_mean_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), 0, s, x, out, HW, C);
     EDGEDET_LAUNCH_CHECK();
     return 0;
@@ -156,6 +159,7 @@ __global__ void se_fc_kernel(const float* __restrict__ mean, const float* __rest
 
 int se_fc_launch(const float* mean, const float* w1t, const float* b1, const float* w2t, const float* b2,
                  float* scale, int B, int C, int S, hipStream_t s) {
+    EDGEDET_REQUIRE(mean && w1t && b1 && w2t && b2 && scale, "se_fc: null pointer");
     const size_t lds = (size_t)(C + S) * sizeof(float);
     EDGEDET_REQUIRE(lds <= 60 * 1024, "se_fc: too many channels");
     hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), lds, s, mean, w1t, b1, w2t, b2, scale, C, S);
@@ -196,6 +200,7 @@ __global__ void maxpool_kernel(PoolParams p) {
 }
 
 int maxpool_launch(const PoolParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.y, "maxpool: null x/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "maxpool: C must be a multiple of 4");
     const int64_t total = (int64_t)p.B * p.Ho * p.Wo * (p.C / 4);
     hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
@@ -205,7 +210,7 @@ int maxpool_launch(const PoolParams& p, hipStream_t s) {
 
 // ------------------------------------------------------------------------------ RoIAlign
 // torchvision roi_align (aligned=False) bilinear_interpolate, restated for NHWC features.
-__device__ __forceinline__ void bilinear_setup(float y, float x, int H, int W, int& o1, int& o2, int& o3, int& o4,
+__host__ __device__ inline void bilinear_setup(float y, float x, int H, int W, int& o1, int& o2, int& o3, int& o4,
                                                float& w1, float& w2, float& w3, float& w4) {
     if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) {
         o1 = o2 = o3 = o4 = 0;
@@ -240,11 +245,10 @@ __device__ __forceinline__ void bilinear_setup(float y, float x, int H, int W, i
 }
 
 
-__global__ void roi_align_kernel(RoiParams p) {
+// One output element group (4 channels of one bin of one RoI).  __host__ __device__ so the exact
+// kernel body also runs in the host-side debug harness (tools/roi_align_host_check.cpp, ASan).
+__host__ __device__ inline void roi_align_thread(const RoiParams& p, int64_t idx) {
     const int C4 = p.C >> 2;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)p.R * p.PH * p.PW * C4;
-    if (idx >= total) return;
     const int c = (int)(idx % C4) * 4;
     int64_t t = idx / C4;
     const int pw = (int)(t % p.PW);
@@ -315,8 +319,17 @@ __global__ void roi_align_kernel(RoiParams p) {
     *reinterpret_cast<f32x4*>(o) = f32x4{acc.x / count, acc.y / count, acc.z / count, acc.w / count};
 }
 
+__global__ void roi_align_kernel(RoiParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.R * p.PH * p.PW * (p.C >> 2);
+    if (idx >= total) return;
+    roi_align_thread(p, idx);
+}
+
 int roi_align_launch(const RoiParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.C % 4 == 0, "roi_align: C must be a multiple of 4");
+    EDGEDET_REQUIRE(p.out != nullptr && p.rois != nullptr && p.feat[0] != nullptr, "roi_align: null pointer");
+    EDGEDET_REQUIRE(p.mode == 0 || (p.counts != nullptr && p.RMAX > 0), "roi_align: mode 1 needs counts/RMAX");
     EDGEDET_REQUIRE(p.nlevels >= 1 && p.nlevels <= 4, "roi_align: 1..4 levels");
     const int64_t total = (int64_t)p.R * p.PH * p.PW * (p.C / 4);
     if (total == 0) return 0;
@@ -346,6 +359,7 @@ extern "C" int edgedet_roi_align(const float* feat, int64_t B, int64_t H, int64_
     p.PH = pooled_h;
     p.PW = pooled_w;
     p.sr = sampling_ratio;
+    p.out = out;
     return roi_align_launch(p, (hipStream_t)stream);
 }
 
