@@ -99,7 +99,7 @@ def op_work(op):
     if k == O.CHANNEL_MEAN:
         return "se_squeeze", float(i[0] * i[1] * i[2]), 4.0 * i[0] * i[1] * i[2]
     if k == O.SE_FC:
-        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * 2 * i[1] * i[2]
+        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * (2 * i[1] * i[2] + i[0] * O.SE_PARTS * i[1])
     if k == O.MAXPOOL:
         B, H, W, C, Ho, Wo = (i[j] for j in range(6))
         return "maxpool", 0.0, 4.0 * (B * H * W * C + B * Ho * Wo * C)
@@ -131,8 +131,13 @@ def per_op_times(plan, stream, reps=20):
     res = []
     recs = plan.records
     sh = O.stream_handle(stream)
+    recs = recs.copy()
+    recs["i"][:, O.LANE_FIELD] = 0  # time every op alone on the timed stream
     with torch.cuda.stream(stream):
         for k in range(len(recs)):
+            if recs[k]["kind"] in (O.FORK, O.JOIN):
+                res.append(0.0)
+                continue
             ptr = recs[k:k + 1].ctypes.data_as(ctypes.c_void_p)
             O.check(L.edgedet_plan_run(ptr, 1, sh))
             e0 = torch.cuda.Event(enable_timing=True)
@@ -146,10 +151,15 @@ def per_op_times(plan, stream, reps=20):
     return res
 
 
-def roofline_for(plan, stream, step_ms):
+OP_DUMP = {}
+
+
+def roofline_for(plan, stream, step_ms, model=""):
     """Dominant kernel family of the step (by measured device time) and its longest launch, priced
     against the roof that binds it (max of flops / fp32-MFMA peak and bytes / HBM peak)."""
     times = per_op_times(plan, stream)
+    OP_DUMP[model] = [{"name": op.name, "family": op_work(op)[0], "ms": round(t, 5), "flops": op_work(op)[1],
+                       "bytes": op_work(op)[2]} for op, t in zip(plan.ops, times)]
     fam = {}
     for op, t in zip(plan.ops, times):
         name = op_work(op)[0]
@@ -230,6 +240,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--dump-ops", default="", help="write the per-op device times of each model to this JSON")
     args = ap.parse_args()
 
     dist, rank, world = dist_setup(args.gpus)
@@ -246,7 +257,7 @@ def main():
         out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
                       "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
         if rank == 0 and not args.no_roofline:
-            out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps)
+            out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps, "ssd")
             attach_traffic(out["ssd"]["roofline"], "ssd")
         del plan
         m.plans.clear()
@@ -264,9 +275,12 @@ def main():
                         "proposals_per_img": R, "dets_per_img": float(plan.out_count.tensor().float().mean().item()),
                         "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2)}
         if rank == 0 and not args.no_roofline:
-            out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps)
+            out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "frcnn")
             attach_traffic(out["frcnn"]["roofline"], "frcnn")
         del plan
+    if rank == 0 and args.dump_ops:
+        with open(args.dump_ops, "w") as f:
+            json.dump(OP_DUMP, f, indent=0)
     if rank != 0:
         if dist:
             dist.destroy_process_group()

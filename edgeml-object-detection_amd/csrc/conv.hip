@@ -15,6 +15,8 @@
 // wave contributes k = 16h + 8q + t (q, t loop indices), so both operands are read from LDS as
 // contiguous f32x4s (ds_read_b128) from K-contiguous rows padded to 36 floats (conflict-free
 // for the b128 lane groups).
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace edgedet {
@@ -24,6 +26,90 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;  // padded LDS row (floats)
+
+// Output offset of GEMM row m (an output pixel), for y (is_res = false) or the residual.
+__device__ __forceinline__ int64_t conv_row_offset(const ConvParams& p, int m, bool is_res) {
+    if (!is_res && p.lin_y) return p.y_off + (int64_t)m * p.y_pstride;
+    if (is_res && p.lin_res) return (int64_t)m * p.res_pstride;
+    const int b = (int)fdiv((uint32_t)m, p.div_howo);
+    const int pix = m - b * p.Ho * p.Wo;
+    if (!is_res) return p.y_off + (int64_t)b * p.y_bstride + (int64_t)pix * p.y_pstride;
+    int rpix = pix;
+    if (p.res_H != p.Ho || p.res_W != p.Wo) {  // FPN top-down: nearest upsample of the residual
+        const int oh = (int)fdiv((uint32_t)pix, p.div_wo);
+        const int ow = pix - oh * p.Wo;
+        int ry = (int)floorf((float)oh * p.res_sh);
+        int rx = (int)floorf((float)ow * p.res_sw);
+        ry = ry < p.res_H - 1 ? ry : p.res_H - 1;
+        rx = rx < p.res_W - 1 ? rx : p.res_W - 1;
+        rpix = ry * p.res_W + rx;
+    }
+    return (int64_t)b * p.res_bstride + (int64_t)rpix * p.res_pstride;
+}
+
+template <int TM, int TN, int ACT>
+__device__ __forceinline__ void act_tile(floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = apply_act(acc[i][j][r], ACT);
+}
+
+// Epilogue shared by both conv kernels.  Row of (i, r) = row0 + 32i + (r&3) + 8(r>>2) + 4h (the
+// 32x32 MFMA C layout), column of j = col0 + 32j + (lane & 31).  Pass 1 adds bias and residual,
+// pass 2 applies the activation (one uniform switch outside the element loops), pass 3 stores.
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16 (&acc)[TM][TN], int row0, int col0,
+                                              int h, int l32) {
+    // Loads use clamped (always valid) rows/columns so no load sits behind a branch; only the
+    // stores are predicated.
+    float bj[TN];
+    int nc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = col0 + j * 32 + l32;
+        nc[j] = n < p.Cout ? n : p.Cout - 1;
+        bj[j] = p.bias[nc[j]];
+    }
+    if (p.res) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = row0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float* rrow = p.res + conv_row_offset(p, m < p.M ? m : p.M - 1, true);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j][r] = (acc[i][j][r] + bj[j]) + rrow[nc[j]];
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] += bj[j];
+    }
+    switch (p.act) {
+        case ACT_RELU: act_tile<TM, TN, ACT_RELU>(acc); break;
+        case ACT_RELU6: act_tile<TM, TN, ACT_RELU6>(acc); break;
+        case ACT_HSWISH: act_tile<TM, TN, ACT_HSWISH>(acc); break;
+        case ACT_HSIGMOID: act_tile<TM, TN, ACT_HSIGMOID>(acc); break;
+        case ACT_SIGMOID: act_tile<TM, TN, ACT_SIGMOID>(acc); break;
+        default: break;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = row0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float* yrow = p.y + conv_row_offset(p, m < p.M ? m : p.M - 1, false);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                if (m < p.M && col0 + j * 32 + l32 < p.Cout) yrow[nc[j]] = acc[i][j][r];
+        }
+}
 
 template <int WM, int WN, int TM, int TN>
 __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
@@ -67,7 +153,13 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
     for (int j = 0; j < AJ; ++j) {
         const int row = (tid >> 3) + (NT / 8) * j;
         const int m = m0 + row;
-        if (m < p.M) {
+        if (m < p.M && p.lin_x) {
+            // 1x1 / stride 1 / pad 0 over a dense NHWC tensor: pixel m sits at m * pstride
+            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_base[j] = (int64_t)m * p.x_pstride;
+            a_ih0[j] = 0;
+            a_iw0[j] = 0;
+        } else if (m < p.M) {
             const int b = (int)fdiv((uint32_t)m, p.div_howo);
             const int rem = m - b * p.Ho * p.Wo;
             const int oh = (int)fdiv((uint32_t)rem, p.div_wo);
@@ -187,41 +279,93 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
         __syncthreads();
     }
 
-    // ---- epilogue: bias + residual + activation, strided store
+    conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pointwise (1x1, stride 1, dense NHWC) conv with operands loaded straight from global memory into
+// MFMA fragments: no LDS, no barriers, four independent waves per block.  For these layers K is small
+// (the narrow MobileNetV3/ResNet 1x1s) and the kernel is bound by HBM, so latency is hidden by wave
+// occupancy instead of LDS staging.  A wave owns a (32*TM) x (32*TN) output tile; lane l supplies
+// row/column (l & 31) and k = 16*(l >> 5) + t of each 32-deep K chunk (t = MFMA step), which for a
+// K-contiguous row is one 64-byte run per lane (a 32-row x 128-byte contiguous block per wave
+// instruction group when Cin == 32).
+template <int TM, int TN>
+__global__ void __launch_bounds__(256) pw_mfma_kernel(ConvParams p) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int nnt = (p.Cout + 32 * TN - 1) / (32 * TN);
+    const int nmt = (p.M + 32 * TM - 1) / (32 * TM);
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wid >= nmt * nnt) return;
+    const int mt = wid / nnt, nt = wid % nnt;  // waves of one block share the A panel
+    const int m0 = mt * 32 * TM, n0 = nt * 32 * TN;
+
+    const float* arow[TM];
+    int ab[TM];
+    bool aval[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int m = m0 + wave_m * TM * 32 + i * 32 + row;
-            if (m >= p.M) continue;
-            const int b = (int)fdiv((uint32_t)m, p.div_howo);
-            const int pix = m - b * p.Ho * p.Wo;
-            float* yrow = p.y + p.y_off + (int64_t)b * p.y_bstride + (int64_t)pix * p.y_pstride;
-            const float* rrow = nullptr;
-            if (p.res) {
-                int rpix = pix;
-                if (p.res_H != p.Ho || p.res_W != p.Wo) {
-                    const int oh = (int)fdiv((uint32_t)pix, p.div_wo);
-                    const int ow = pix - oh * p.Wo;
-                    int ry = (int)floorf((float)oh * p.res_sh);
-                    int rx = (int)floorf((float)ow * p.res_sw);
-                    ry = ry < p.res_H - 1 ? ry : p.res_H - 1;
-                    rx = rx < p.res_W - 1 ? rx : p.res_W - 1;
-                    rpix = ry * p.res_W + rx;
-                }
-                rrow = p.res + (int64_t)b * p.res_bstride + (int64_t)rpix * p.res_pstride;
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wave_n * TN * 32 + j * 32 + l32;
-                if (n >= p.Cout) continue;
-                float v = acc[i][j][r] + p.bias[n];
-                if (rrow) v += rrow[n];
-                yrow[n] = apply_act(v, p.act);
-            }
-        }
+        const int m = m0 + i * 32 + l32;
+        aval[i] = m < p.M;
+        arow[i] = p.x + (int64_t)(aval[i] ? m : 0) * p.x_pstride;
+        ab[i] = (p.in_scale && aval[i]) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
     }
+    const float* brow[TN];
+    bool bval[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 32 + l32;
+        bval[j] = n < p.Cout;
+        brow[j] = p.w + (int64_t)(bval[j] ? n : 0) * p.Kpad;
+    }
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    for (int k0 = 0; k0 < p.Kpad; k0 += 32) {
+        const int kk = k0 + 16 * h;
+        f32x4 a[TM][4], b[TN][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = kk + 4 * q;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (aval[i] && k < p.K) {
+                    v = *reinterpret_cast<const f32x4*>(arow[i] + k);
+                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)ab[i] * p.Cin + k);
+                }
+                a[i][q] = v;
+            }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                b[j][q] = bval[j] ? *reinterpret_cast<const f32x4*>(brow[j] + kk + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t >> 2][t & 3], b[j][t >> 2][t & 3],
+                                                                      acc[i][j], 0, 0, 0);
+    }
+    conv_epilogue<TM, TN>(p, acc, m0, n0, h, l32);
+}
+
+template <int TM, int TN>
+static int launch_pw(const ConvParams& p, hipStream_t s) {
+    const int64_t waves = cdiv(p.M, 32 * TM) * cdiv(p.Cout, 32 * TN);
+    EDGEDET_REQUIRE(waves < (1ll << 31), "pw conv grid too large");
+    hipLaunchKernelGGL((pw_mfma_kernel<TM, TN>), dim3((unsigned)cdiv(waves, 4)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
 }
 
 template <int WM, int WN, int TM, int TN>
@@ -232,6 +376,34 @@ static int launch_cfg(const ConvParams& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, TM, TN>), dim3((unsigned)nwg), dim3(WM * WN * 64), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
+}
+
+// Tile choice: the direct pointwise kernel for narrow-K 1x1 layers (HBM-bound, no reuse to stage);
+// otherwise the largest LDS-staged tile that still gives about one workgroup per CU.
+static int big_tile_override() {
+    static const int v = [] {
+        const char* e = std::getenv("EDGEDET_BIG_TILE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+static int choose_tile(const ConvParams& p) {
+    if (big_tile_override() && (int64_t)p.M >= 65536 && p.Cout >= 128 && p.Kpad >= 512) return big_tile_override();
+    if (p.lin_x && (p.Kpad <= 128 || p.Cout <= 32)) {
+        if (p.Cout <= 32) return 11;
+        const int64_t w22 = cdiv(p.M, 64) * cdiv(p.Cout, 64);
+        return w22 >= 4 * 256 ? 10 : 12;
+    }
+    struct C { int tile, bm, bn; };
+    const C cands_wide[] = {{3, 128, 128}, {2, 128, 64}, {5, 64, 64}, {6, 32, 32}};
+    const C cands_mid[] = {{2, 128, 64}, {5, 64, 64}, {6, 32, 32}};
+    const C cands_narrow[] = {{1, 128, 32}, {6, 32, 32}};
+    const C* c = p.Cout > 64 ? cands_wide : (p.Cout > 32 ? cands_mid : cands_narrow);
+    const int nc = p.Cout > 64 ? 4 : (p.Cout > 32 ? 3 : 2);
+    for (int i = 0; i < nc; ++i)
+        if (cdiv(p.M, c[i].bm) * cdiv(p.Cout, c[i].bn) >= 240) return c[i].tile;
+    return c[nc - 1].tile;
 }
 
 // Host launcher shared by the plan executor and the unit C entry point.
@@ -251,12 +423,27 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
     if (p.res_W <= 0) p.res_W = p.Wo;
     p.res_sh = (float)p.res_H / (float)p.Ho;
     p.res_sw = (float)p.res_W / (float)p.Wo;
-    if (tile <= 0) tile = p.Cout <= 32 ? 1 : (p.Cout <= 64 ? 2 : 3);
+    p.lin_x = (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.pad == 0 && p.Ho == p.H && p.Wo == p.W &&
+               p.x_bstride == (int64_t)p.H * p.W * p.x_pstride) ? 1 : 0;
+    p.lin_y = (p.y_bstride == (int64_t)p.Ho * p.Wo * p.y_pstride) ? 1 : 0;
+    p.lin_res = (p.res_H == p.Ho && p.res_W == p.Wo && p.res_bstride == (int64_t)p.Ho * p.Wo * p.res_pstride) ? 1 : 0;
+    if (tile <= 0) tile = choose_tile(p);
     switch (tile) {
         case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
         case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
         case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128
         case 4: return launch_cfg<4, 2, 2, 2>(p, s);  // 256 x 128
+        case 5: return launch_cfg<2, 2, 1, 1>(p, s);  // 64 x 64
+        case 6: return launch_cfg<1, 1, 1, 1>(p, s);  // 32 x 32 (one wave)
+        case 10:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw<2, 2>(p, s);               // direct, 64 x 64 per wave
+        case 11:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw<4, 1>(p, s);               // direct, 128 x 32 per wave
+        case 12:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw<1, 2>(p, s);               // direct, 32 x 64 per wave
         default: EDGEDET_REQUIRE(false, "conv: unknown tile config");
     }
 }

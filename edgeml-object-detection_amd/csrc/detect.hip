@@ -26,6 +26,9 @@
 //      candidates at a time;
 //   5. kept records (box, score, tiebreak, label) are written to per-segment lists that
 //      merge_topk combines per image.
+#include <cmath>
+#include <cstring>
+#include <limits>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -67,26 +70,54 @@ __device__ __forceinline__ f32x4 clip_box(f32x4 b, float h, float w) {
 }
 
 // ================================================================ SSD: softmax + decode + clip
-// One thread per anchor.  logits [B][A][NC] -> scores_t [B][NC][A] (class-major for the per-class
-// selection), reg [B][A][4] + anchors [A][4] -> boxes [B][A][4].
-__global__ void ssd_scores_kernel(const float* __restrict__ logits, const float* __restrict__ reg,
-                                  const float* __restrict__ anchors, float* __restrict__ scores_t,
-                                  float* __restrict__ boxes, int B, int A, int NC, float img_h, float img_w) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)B * A) return;
-    const int b = (int)(idx / A), a = (int)(idx % A);
-    const float* l = logits + idx * NC;
-    float mx = l[0];
-    for (int c = 1; c < NC; ++c) mx = fmaxf(mx, l[c]);
+// Block = 64 consecutive anchors x 4 waves.  The 64 x NC logits tile is one contiguous span: it is
+// loaded coalesced into LDS (odd row pitch: conflict-free column reads); wave q reduces classes
+// c = q (mod 4) of all 64 anchors, and writes them class-major (scores_t [B][NC][A]: 64 consecutive
+// anchors per store, coalesced) for the per-class selection.  reg [B][A][4] + anchors [A][4] ->
+// boxes [B][A][4] (decode + clip) by wave 0.
+constexpr int SSD_MAXNC = 128;
+
+__global__ void __launch_bounds__(256) ssd_scores_kernel(const float* __restrict__ logits, const float* __restrict__ reg,
+                                                         const float* __restrict__ anchors, float* __restrict__ scores_t,
+                                                         float* __restrict__ boxes, int B, int A, int NC, float img_h,
+                                                         float img_w) {
+    __shared__ float tile[64 * (SSD_MAXNC + 1)];
+    __shared__ float red[4][64];
+    const int b = blockIdx.y;
+    const int a0 = blockIdx.x * 64;
+    const int na = min(64, A - a0);
+    const int ld = (NC & 1) ? NC : NC + 1;
+    const float* src = logits + ((int64_t)b * A + a0) * NC;
+    for (int e = threadIdx.x; e < na * NC; e += 256) {
+        const int a = e / NC, c = e - a * NC;
+        tile[a * ld + c] = src[e];
+    }
+    __syncthreads();
+    const int a = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const float* row = tile + a * ld;
+    float mx = -__builtin_inff();
+    for (int c = q; c < NC; c += 4) mx = fmaxf(mx, row[c]);
+    red[q][a] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0][a], red[1][a]), fmaxf(red[2][a], red[3][a]));
+    __syncthreads();
     float sum = 0.f;
-    for (int c = 0; c < NC; ++c) sum += expf(l[c] - mx);
+    for (int c = q; c < NC; c += 4) sum += expf(row[c] - mx);
+    red[q][a] = sum;
+    __syncthreads();
+    sum = ((red[0][a] + red[1][a]) + red[2][a]) + red[3][a];
     const float inv = 1.f / sum;
-    float* st = scores_t + (int64_t)b * NC * A + a;
-    for (int c = 0; c < NC; ++c) st[(int64_t)c * A] = expf(l[c] - mx) * inv;
-    const f32x4 d = *reinterpret_cast<const f32x4*>(reg + idx * 4);
-    const f32x4 an = *reinterpret_cast<const f32x4*>(anchors + (int64_t)a * 4);
-    f32x4 bx = decode_box(d, an, 10.f, 10.f, 5.f, 5.f);
-    *reinterpret_cast<f32x4*>(boxes + idx * 4) = clip_box(bx, img_h, img_w);
+    if (a < na) {
+        float* st = scores_t + (int64_t)b * NC * A + a0 + a;
+        for (int c = q; c < NC; c += 4) st[(int64_t)c * A] = expf(row[c] - mx) * inv;
+        if (q == 0) {
+            const int64_t idx = (int64_t)b * A + a0 + a;
+            const f32x4 d = *reinterpret_cast<const f32x4*>(reg + idx * 4);
+            const f32x4 an = *reinterpret_cast<const f32x4*>(anchors + (int64_t)(a0 + a) * 4);
+            f32x4 bx = decode_box(d, an, 10.f, 10.f, 5.f, 5.f);
+            *reinterpret_cast<f32x4*>(boxes + idx * 4) = clip_box(bx, img_h, img_w);
+        }
+    }
 }
 
 // ================================================================ FRCNN RoIHeads: softmax + decode
@@ -154,7 +185,7 @@ struct SegSmem {
     int aux[KC];                           // sort payload / group ids
     unsigned int hist[256];
     int wsum[32];
-    int misc[8];
+    int misc[32];
     unsigned char valid[KC];
 };
 
@@ -222,6 +253,70 @@ __device__ uint32_t radix_select(int n, int K, F fkey, unsigned int* hist, int* 
     return prefix;
 }
 
+// Register-resident top-K selection (no atomics).  Element i = threadIdx.x + NT*j lives in
+// kr[j] (key 0 = invalid; valid keys must be > 0).  The K-th largest key T is found by bisection on
+// the key space: each probe counts keys >= t with one ballot + popcount per register (wave totals
+// in SGPRs) and one barrier.  Then ordered compaction writes every key > T plus the first ties
+// == T in index order (the reference's stable order) into keys[] (at most cap).  Returns the count.
+template <int NT>
+__device__ __forceinline__ int block_sum_uniform(int wave_val, int* red) {
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wave_val;
+    __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) tot += red[w];
+    __syncthreads();
+    return tot;
+}
+
+template <int NT, int PER>
+__device__ __forceinline__ int count_ge(const uint32_t (&kr)[PER], uint32_t t, int* red) {
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) c += __popcll(__ballot(kr[j] >= t));
+    return block_sum_uniform<NT>(c, red);
+}
+
+template <int NT, int PER>
+__device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsigned long long* keys, int* wsum,
+                                int* red, bool all_ties = false) {
+    const int nvalid = count_ge<NT, PER>(kr, 1u, red);
+    uint32_t T = 1u;
+    int need_eq = 0;
+    const bool take_all = nvalid <= K;
+    if (!take_all) {
+        uint64_t lo = 1, hi = 1ull << 32;  // count(>= lo) >= K > count(>= hi)
+        while (hi - lo > 1) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (count_ge<NT, PER>(kr, (uint32_t)mid, red) >= K) lo = mid;
+            else hi = mid;
+        }
+        T = (uint32_t)lo;
+        const int greater = (hi >> 32) ? 0 : count_ge<NT, PER>(kr, (uint32_t)hi, red);
+        need_eq = all_ties ? cap : K - greater;
+    }
+    int written = 0, eq_taken = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t k = kr[j];
+        const bool gt = take_all ? (k >= 1u) : (k > T);
+        const bool eq = !take_all && k == T;
+        int tot_gt, tot_eq;
+        const int pos_gt = BlockScan<NT>::exclusive(gt ? 1 : 0, wsum, tot_gt);
+        const int pos_eq = BlockScan<NT>::exclusive(eq ? 1 : 0, wsum, tot_eq);
+        const int budget = need_eq - eq_taken;
+        const uint32_t i = threadIdx.x + (uint32_t)NT * j;
+        if (gt && written + pos_gt < cap) keys[written + pos_gt] = make_key(k, i);
+        if (eq && pos_eq < budget && written + tot_gt + pos_eq < cap)
+            keys[written + tot_gt + pos_eq] = make_key(k, i);
+        const int eq_used = tot_eq < budget ? tot_eq : (budget > 0 ? budget : 0);
+        written += tot_gt + eq_used;
+        eq_taken += eq_used;
+    }
+    __syncthreads();
+    return written < cap ? written : cap;
+}
+
 // Ordered compaction into keys[]: every valid key > T (all valid when take_all) plus the first
 // `eq_budget` keys == T in index order; at most `cap` written.  Returns the count.
 template <int NT, typename F>
@@ -287,8 +382,13 @@ __device__ void bitonic_desc(unsigned long long* keys, int* payload, int m) {
     }
 }
 
-// IoU test in the op order of torchvision's CPU nms kernel; the float IoU is compared in double.
-__device__ __forceinline__ bool iou_gt(f32x4 a, float area_a, f32x4 b, float area_b, double thr) {
+// IoU threshold test, bit-exact with torchvision's CPU nms: `(double)RN_f32(inter / uni) > thr`, where
+// inter and uni = (area_i + area_j) - inter are computed in float in the reference's op order.  The
+// float division is replaced by an exact comparison: with t1 = the smallest float > thr and t0 its
+// predecessor, RN(x) > thr <=> x > mid(t0, t1), or x == mid and round-half-even picks t1.  mid has
+// <= 25 significant bits, so mid * uni is exact in double and so is the comparison (uni > 0; other
+// cases keep the division).  See make_iou_thr.
+__device__ __forceinline__ bool iou_gt(f32x4 a, float area_a, f32x4 b, float area_b, const IouThr& t) {
     const float xx1 = fmaxf(a.x, b.x), yy1 = fmaxf(a.y, b.y);
     const float xx2 = fminf(a.z, b.z), yy2 = fminf(a.w, b.w);
     float w = xx2 - xx1;
@@ -296,15 +396,19 @@ __device__ __forceinline__ bool iou_gt(f32x4 a, float area_a, f32x4 b, float are
     float h = yy2 - yy1;
     h = h > 0.f ? h : 0.f;
     const float inter = w * h;
-    const float ovr = inter / ((area_a + area_b) - inter);
-    return (double)ovr > thr;
+    const float uni = (area_a + area_b) - inter;
+    if (uni > 0.f) {
+        const double dl = (double)inter, dr = t.mid * (double)uni;
+        return dl > dr || (dl == dr && t.tie_up);
+    }
+    return (double)(inter / uni) > t.thr;
 }
 
 // Greedy NMS over S.box[0..m) in sorted order.  In: S.valid = candidate may be kept (invalid ones
 // neither survive nor suppress).  Out: S.valid = kept.  If `groups`, only pairs with equal
 // S.aux[] group ids interact (batched_nms).
 template <int NT, int KC>
-__device__ void nms_block(SegSmem<KC>& S, int m, double thr, bool groups) {
+__device__ void nms_block(SegSmem<KC>& S, int m, const IouThr& thr, bool groups) {
     constexpr int NWORDS = KC / 64;
     const int nw = (m + 63) >> 6;
     for (int t = threadIdx.x; t < m * nw; t += NT) {
@@ -386,38 +490,147 @@ __device__ void write_kept(SegSmem<KC>& S, int m, int seg, const SegOut& out, W 
     if (threadIdx.x == 0) out.count[seg] = written < out.kmax ? written : out.kmax;
 }
 
-// ================================================================ SSD per-class selection
-// grid (NC-1, B): candidates = anchors with score > score_thresh, top `topk`, NMS.
-template <int NT, int KC>
-__global__ void __launch_bounds__(NT) ssd_class_nms_kernel(const float* __restrict__ scores_t,
-                                                           const f32x4* __restrict__ boxes, int A, int NC,
-                                                           float score_thresh, int topk, double iou, SegOut out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
-    const int c = blockIdx.x + 1;  // class 0 is background
+// ================================================================ SSD per-class selection, wave form
+// One wave per (image, class), four independent waves per workgroup and no workgroup barriers:
+//   select   scores live in VGPRs (element i = lane + 64*j); the top-k threshold is found by
+//            bisection with one ballot + popcount per register per probe;
+//   compact  in index order (j-major, then lane) with ballots and lane masks: ties at the threshold
+//            are taken lowest index first (the reference's stable order);
+//   sort     wave-synchronous bitonic sort of (score, ~index) keys in this wave's LDS slice;
+//   NMS      lazy greedy: the earliest candidate still alive is kept and suppresses the alive
+//            candidates it overlaps (IoU over register-resident boxes, 64 lanes x KC/64 each); only
+//            kept candidates' rows are ever evaluated, in sorted order, as the reference's loop does.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int PER, int KC>
+__global__ void __launch_bounds__(256) ssd_class_nms_wave_kernel(const float* __restrict__ scores_t,
+                                                                 const f32x4* __restrict__ boxes, int A, int NC,
+                                                                 float score_thresh, int topk, IouThr iou,
+                                                                 SegOut out) {
+    constexpr int NQ = KC / 64;
+    __shared__ unsigned long long keys_s[4][KC];
+    __shared__ f32x4 box_s[4][KC];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + w + 1;  // class 0 is background
     const int b = blockIdx.y;
+    if (c >= NC) return;                   // whole wave leaves; nothing below waits on other waves
+    unsigned long long* keys = keys_s[w];
+    f32x4* bs = box_s[w];
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const float* sc = scores_t + ((int64_t)b * NC + c) * A;
-    auto fkey = [&](int i, uint32_t& k) -> bool {
-        const float s = sc[i];
-        k = __float_as_uint(s);  // probabilities are >= 0: raw bits are ordered
-        return s > score_thresh;
-    };
-    const uint32_t T = radix_select<NT>(A, topk, fkey, S.hist, S.misc);
-    const bool take_all = S.misc[1] <= topk;
-    const int m = compact<NT>(A, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
-    bitonic_desc<NT>(S.keys, nullptr, m);
-    for (int t = threadIdx.x; t < m; t += NT) {
-        S.box[t] = boxes[(int64_t)b * A + key_index(S.keys[t])];
-        S.valid[t] = 1;
+
+    uint32_t kr[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int i = lane + 64 * j;
+        const float v = i < A ? sc[i] : 0.f;
+        kr[j] = (i < A && v > score_thresh) ? __float_as_uint(v) : 0u;  // probabilities >= 0: bits ordered
     }
-    __syncthreads();
-    nms_block<NT, KC>(S, m, iou, false);
-    write_kept<NT, KC>(S, m, b * (NC - 1) + (c - 1), out, [&](int t, int64_t o) {
-        out.box[o] = S.box[t];
-        out.score[o] = __uint_as_float((uint32_t)(S.keys[t] >> 32));
-        out.tb[o] = ((uint32_t)c << 16) | (uint32_t)t;  // concatenation order: (class, rank)
-        out.label[o] = c;
-    });
+    auto count_ge = [&](uint32_t t) -> int {
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) n += __popcll(__ballot(kr[j] >= t));
+        return n;
+    };
+    const int nvalid = count_ge(1u);
+    const bool take_all = nvalid <= topk;
+    uint32_t T = 1u;
+    int need_eq = 0;
+    if (!take_all) {
+        uint64_t lo = 1, hi = 1ull << 32;
+        while (hi - lo > 1) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            if (count_ge((uint32_t)mid) >= topk) lo = mid;
+            else hi = mid;
+        }
+        T = (uint32_t)lo;
+        need_eq = topk - ((hi >> 32) ? 0 : count_ge((uint32_t)hi));
+    }
+    int written = 0, eq_taken = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t k = kr[j];
+        const bool gt = take_all ? (k != 0u) : (k > T);
+        const bool eq = !take_all && k == T;
+        const unsigned long long mg = __ballot(gt), me = __ballot(eq);
+        const int ng = __popcll(mg), ne = __popcll(me);
+        const int budget = need_eq - eq_taken;
+        const uint32_t i = (uint32_t)(lane + 64 * j);
+        if (gt) {
+            const int slot = written + __popcll(mg & lt_mask);
+            if (slot < KC) keys[slot] = make_key(k, i);
+        }
+        if (eq) {
+            const int pe = __popcll(me & lt_mask);
+            const int slot = written + ng + pe;
+            if (pe < budget && slot < KC) keys[slot] = make_key(k, i);
+        }
+        const int used = ne < budget ? ne : (budget > 0 ? budget : 0);
+        written += ng + used;
+        eq_taken += used;
+    }
+    const int m = written < KC ? written : KC;
+    int p2 = 64;
+    while (p2 < m) p2 <<= 1;
+    for (int i = m + lane; i < p2; i += 64) keys[i] = 0ull;
+    wave_sync();
+    for (int k = 2; k <= p2; k <<= 1) {
+        for (int jd = k >> 1; jd > 0; jd >>= 1) {
+            for (int t = lane; t < p2 / 2; t += 64) {
+                const int i = 2 * t - (t & (jd - 1));
+                const int l = i + jd;
+                const bool desc = (i & k) == 0;
+                const unsigned long long x = keys[i], y = keys[l];
+                if ((x < y) == desc) {
+                    keys[i] = y;
+                    keys[l] = x;
+                }
+            }
+            wave_sync();
+        }
+    }
+    for (int t = lane; t < m; t += 64) bs[t] = boxes[(int64_t)b * A + key_index(keys[t])];
+    wave_sync();
+    f32x4 bq[NQ];
+    float aq[NQ];
+    uint32_t alive = 0u;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int j = lane + 64 * q;
+        bq[q] = j < m ? bs[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+        aq[q] = (bq[q].z - bq[q].x) * (bq[q].w - bq[q].y);
+        if (j < m) alive |= 1u << q;
+    }
+    const int seg = b * (NC - 1) + (c - 1);
+    int nkept = 0;
+    while (true) {
+        int i = -1;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const unsigned long long mq = __ballot((alive >> q) & 1u);
+            if (i < 0 && mq) i = 64 * q + __builtin_ctzll(mq);
+        }
+        if (i < 0) break;
+        if (lane == (i & 63)) alive &= ~(1u << (i >> 6));
+        const f32x4 bi = bs[i];
+        const float ai = (bi.z - bi.x) * (bi.w - bi.y);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            if (((alive >> q) & 1u) && iou_gt(bi, ai, bq[q], aq[q], iou)) alive &= ~(1u << q);
+        if (lane == 0 && nkept < out.kmax) {
+            const int64_t o = (int64_t)seg * out.kmax + nkept;
+            out.box[o] = bi;
+            out.score[o] = __uint_as_float((uint32_t)(keys[i] >> 32));
+            out.tb[o] = ((uint32_t)c << 16) | (uint32_t)i;  // concatenation order: (class, rank)
+            out.label[o] = c;
+        }
+        ++nkept;
+    }
+    if (lane == 0) out.count[seg] = nkept < out.kmax ? nkept : out.kmax;
 }
 
 // ================================================================ RPN per-level selection
@@ -428,11 +641,10 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
     SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
     const int l = blockIdx.x, b = blockIdx.y;
     const RpnLevel L = P.lv[l];
-    const int HW = L.n / P.A;
-    const float* hb = L.head + (int64_t)b * HW * P.ld;
+    const float* ob = L.obj + (int64_t)b * L.n;
+    const f32x4* db = reinterpret_cast<const f32x4*>(L.deltas) + (int64_t)b * L.n;
     auto fkey = [&](int i, uint32_t& k) -> bool {
-        const int pix = i / P.A, a = i - pix * P.A;
-        k = float_key(hb[(int64_t)pix * P.ld + a]);
+        k = float_key(ob[i]);
         return true;
     };
     const uint32_t T = radix_select<NT>(L.n, P.topk, fkey, S.hist, S.misc);
@@ -441,9 +653,7 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
     bitonic_desc<NT>(S.keys, nullptr, m);
     for (int t = threadIdx.x; t < m; t += NT) {
         const int i = key_index(S.keys[t]);
-        const int pix = i / P.A, a = i - pix * P.A;
-        const float* row = hb + (int64_t)pix * P.ld + P.A + 4 * a;
-        const f32x4 d = f32x4{row[0], row[1], row[2], row[3]};
+        const f32x4 d = db[i];
         const f32x4 an = *reinterpret_cast<const f32x4*>(L.anchors + (int64_t)i * 4);
         const f32x4 bx = clip_box(decode_box(d, an, 1.f, 1.f, 1.f, 1.f), P.img_h, P.img_w);
         const float logit = key_float((uint32_t)(S.keys[t] >> 32));
@@ -467,7 +677,7 @@ template <int NT, int KC>
 __global__ void __launch_bounds__(NT) box_class_nms_kernel(const float* __restrict__ scores,
                                                            const f32x4* __restrict__ boxes,
                                                            const int* __restrict__ counts, int R, int NC,
-                                                           float score_thresh, float min_size, double iou,
+                                                           float score_thresh, float min_size, IouThr iou,
                                                            SegOut out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
@@ -502,7 +712,7 @@ __global__ void __launch_bounds__(NT) box_class_nms_kernel(const float* __restri
 // ================================================================ unit (batched) NMS for the C API
 template <int NT, int KC>
 __global__ void __launch_bounds__(NT) unit_nms_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
-                                                      const int64_t* __restrict__ idxs, int n, double iou,
+                                                      const int64_t* __restrict__ idxs, int n, IouThr iou,
                                                       int64_t* __restrict__ keep, int* __restrict__ num_keep) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
@@ -535,28 +745,62 @@ __global__ void __launch_bounds__(NT) unit_nms_kernel(const float* __restrict__ 
 // ================================================================ per-image merge
 // Kept lists [B][S][kmax] -> top N by (score desc, tiebreak asc), boxes rescaled by ratio.
 
-template <int NT, int KC>
+template <int NT, int KC, int PER>
 __global__ void __launch_bounds__(NT) merge_topk_kernel(MergeParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
     const int b = blockIdx.x;
-    const int n = P.S * P.kmax;
     const int* cnt = P.count + (int64_t)b * P.S;
     const int64_t base_off = (int64_t)b * P.S * P.kmax;
-    auto fkey = [&](int i, uint32_t& k) -> bool {
-        const int s = i / P.kmax, slot = i - s * P.kmax;
-        if (slot >= cnt[s]) return false;
-        k = __float_as_uint(P.score[base_off + i]);  // scores >= 0
-        return true;
+    // candidates = the valid prefix [0, count) of every segment, concatenated in segment order
+    int* pre = S.aux;  // pre[s] = first candidate of segment s, pre[S] = total
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int q = 0; q < P.S; ++q) {
+            pre[q] = acc;
+            const int c = cnt[q];
+            acc += c < P.kmax ? c : P.kmax;
+        }
+        pre[P.S] = acc;
+    }
+    __syncthreads();
+    const int n = pre[P.S];
+    auto flat = [&](int i) -> int {  // candidate index -> segment * kmax + slot
+        int lo = 0, hi = P.S;        // largest q with pre[q] <= i
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return lo * P.kmax + (i - pre[lo]);
     };
-    const uint32_t T = radix_select<NT>(n, P.N, fkey, S.hist, S.misc);
-    const bool take_all = S.misc[1] <= P.N;
-    // every key > T plus all ties (up to capacity); ties are ordered by tiebreak in the sort
-    const int m0 = compact<NT>(n, T, take_all, KC, KC, fkey, S.keys, S.wsum);
+    int m0;
+    if (n <= NT * PER) {
+        uint32_t kr[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = threadIdx.x + NT * j;
+            kr[j] = i < n ? float_key(P.score[base_off + flat(i)]) : 0u;
+        }
+        // every key > T plus all ties (up to capacity); ties are then ordered by tiebreak
+        m0 = select_topk_regs<NT, PER>(kr, P.N, KC, S.keys, S.wsum, S.misc, true);
+    } else {
+        auto fkey = [&](int i, uint32_t& k) -> bool {
+            k = float_key(P.score[base_off + flat(i)]);
+            return true;
+        };
+        const uint32_t T = radix_select<NT>(n, P.N, fkey, S.hist, S.misc);
+        const bool take_all = S.misc[1] <= P.N;
+        m0 = compact<NT>(n, T, take_all, KC, KC, fkey, S.keys, S.wsum);
+    }
+    // candidate indices must be recovered before pre[] (aliasing aux) is overwritten
+    unsigned long long* tmp = S.mask;
+    for (int t = threadIdx.x; t < m0; t += NT) tmp[t] = (unsigned long long)flat(key_index(S.keys[t]));
+    __syncthreads();
     for (int t = threadIdx.x; t < m0; t += NT) {
-        const int i = key_index(S.keys[t]);
-        S.aux[t] = i;
-        S.keys[t] = make_key(__float_as_uint(P.score[base_off + i]), P.tb[base_off + i]);
+        const int f = (int)tmp[t];
+        S.aux[t] = f;
+        S.keys[t] = make_key(__float_as_uint(P.score[base_off + f]), P.tb[base_off + f]);
     }
     __syncthreads();
     bitonic_desc<NT>(S.keys, S.aux, m0);
@@ -606,8 +850,8 @@ static bool seg_ok(const SegOut& o) { return o.box && o.score && o.tb && o.label
 int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,
                       int B, int A, int NC, float img_h, float img_w, hipStream_t s) {
     EDGEDET_REQUIRE(logits && reg && anchors && scores_t && boxes, "ssd_scores: null pointer");
-    const int64_t total = (int64_t)B * A;
-    hipLaunchKernelGGL(ssd_scores_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, logits, reg, anchors,
+    EDGEDET_REQUIRE(NC <= SSD_MAXNC, "ssd_scores: at most 128 classes");
+    hipLaunchKernelGGL(ssd_scores_kernel, dim3((unsigned)cdiv(A, 64), B), dim3(256), 0, s, logits, reg, anchors,
                        scores_t, boxes, B, A, NC, img_h, img_w);
     EDGEDET_LAUNCH_CHECK();
     return 0;
@@ -624,15 +868,27 @@ int box_scores_launch(const float* pred, int ld, int cls_off, int delta_off, con
     return 0;
 }
 
+IouThr make_iou_thr(double thr) {
+    IouThr t;
+    t.thr = thr;
+    float t1 = (float)thr;
+    if ((double)t1 <= thr) t1 = std::nextafter(t1, std::numeric_limits<float>::infinity());
+    const float t0 = std::nextafter(t1, -std::numeric_limits<float>::infinity());
+    t.mid = ((double)t0 + (double)t1) * 0.5;
+    uint32_t bits;
+    std::memcpy(&bits, &t1, 4);
+    t.tie_up = (bits & 1u) == 0u;
+    return t;
+}
+
 int ssd_class_nms_launch(const float* scores_t, const float* boxes, int B, int A, int NC, float score_thresh,
                          int topk, double iou, SegOut out, hipStream_t s) {
     EDGEDET_REQUIRE(scores_t && boxes && seg_ok(out), "ssd_class_nms: null pointer");
     EDGEDET_REQUIRE(topk <= 512 && out.kmax >= topk, "ssd_class_nms: topk must be <= 512 and <= kmax");
-    constexpr int KC = 512, NT = 256;
-    auto k = ssd_class_nms_kernel<NT, KC>;
-    if (set_lds(k, seg_smem<KC>())) return -2;
-    hipLaunchKernelGGL(k, dim3(NC - 1, B), dim3(NT), seg_smem<KC>(), s, scores_t, (const f32x4*)boxes, A, NC,
-                       score_thresh, topk, iou, out);
+    constexpr int KC = 512, PER = 52;
+    EDGEDET_REQUIRE(A <= 64 * PER, "ssd_class_nms: at most 3328 anchors per image");
+    hipLaunchKernelGGL((ssd_class_nms_wave_kernel<PER, KC>), dim3((unsigned)cdiv(NC - 1, 4), B), dim3(256), 0, s,
+                       scores_t, (const f32x4*)boxes, A, NC, score_thresh, topk, make_iou_thr(iou), out);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -642,7 +898,7 @@ int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s) {
     EDGEDET_REQUIRE(P.nlevels >= 1 && P.nlevels <= 5, "rpn: 1..5 levels");
     EDGEDET_REQUIRE(seg_ok(out), "rpn: null output records");
     for (int l = 0; l < P.nlevels; ++l)
-        EDGEDET_REQUIRE(P.lv[l].head && P.lv[l].anchors && P.lv[l].n > 0, "rpn: null/empty level");
+        EDGEDET_REQUIRE(P.lv[l].obj && P.lv[l].deltas && P.lv[l].anchors && P.lv[l].n > 0, "rpn: null/empty level");
     constexpr int KC = 1024, NT = 512;
     auto k = rpn_level_nms_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;
@@ -659,7 +915,7 @@ int box_class_nms_launch(const float* scores, const float* boxes, const int* cou
     auto k = box_class_nms_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;
     hipLaunchKernelGGL(k, dim3(NC - 1, B), dim3(NT), seg_smem<KC>(), s, scores, (const f32x4*)boxes, counts, R, NC,
-                       score_thresh, min_size, iou, out);
+                       score_thresh, min_size, make_iou_thr(iou), out);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -668,8 +924,9 @@ int merge_topk_launch(const MergeParams& P, int B, hipStream_t s) {
     EDGEDET_REQUIRE(P.box && P.score && P.tb && P.label && P.count && P.out_box && P.out_score && P.out_count,
                     "merge_topk: null pointer");
     EDGEDET_REQUIRE(P.N <= 1024 && P.N > 0 && P.S > 0 && P.kmax > 0, "merge_topk: bad sizes");
-    constexpr int KC = 1024, NT = 512;
-    auto k = merge_topk_kernel<NT, KC>;
+    EDGEDET_REQUIRE(P.S < 1024, "merge_topk: at most 1023 segments");
+    constexpr int KC = 1024, NT = 512, PER = 64;
+    auto k = merge_topk_kernel<NT, KC, PER>;
     if (set_lds(k, seg_smem<KC>())) return -2;
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), seg_smem<KC>(), s, P);
     EDGEDET_LAUNCH_CHECK();
@@ -693,7 +950,8 @@ extern "C" int edgedet_batched_nms(const float* boxes, const float* scores, cons
     auto k = unit_nms_kernel<NT, KC>;
     const size_t lds = seg_smem<KC>();
     if (set_lds(k, lds)) return -2;
-    hipLaunchKernelGGL(k, dim3(1), dim3(NT), lds, s, boxes, scores, idxs, (int)n, iou_threshold, keep, d_num_keep);
+    hipLaunchKernelGGL(k, dim3(1), dim3(NT), lds, s, boxes, scores, idxs, (int)n, make_iou_thr(iou_threshold), keep,
+                       d_num_keep);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

@@ -13,8 +13,8 @@
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act
-//   CHANNEL_MEAN   p0 x[B,HW,C]; p1 out[B,C]; i0..2 B,HW,C
-//   SE_FC          p0 mean; p1 w1t[C][S]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; i0..2 B,C,S
+//   CHANNEL_MEAN   p0 x[B,HW,C]; p1 part[B,16,C] (partial sums over 16 pixel splits); i0..2 B,HW,C
+//   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; i0..3 B,C,S,HW
 //   MAXPOOL        p0 x; p1 y; i0..8 B,H,W,C,Ho,Wo,K,stride,pad
 //   SSD_SCORES     p0 logits[B,A,NC]; p1 reg[B,A,4]; p2 anchors[A,4]; p3 scores_t[B,NC,A];
 //                  p4 boxes[B,A,4]; i0..2 B,A,NC; f0,f1 img_h,img_w
@@ -22,8 +22,8 @@
 //                  i0..4 B,A,NC,topk,kmax; f0 score_thresh; d0 iou
 //   MERGE_TOPK     p0..4 records; p5 ratio[B,2]|0; p6 out_box; p7 out_score; p8 out_label|0;
 //                  p9 out_count; i0..3 B,S,kmax,N
-//   RPN_LEVEL_NMS  p0..4 head per level; p5..9 anchors per level; p10..14 records;
-//                  i0..5 B,nlevels,ld,A,topk,kmax; i6..10 n per level;
+//   RPN_LEVEL_NMS  p0..4 objectness [B][n] per level; p5..9 anchors per level; p10..14 records;
+//                  p15..19 deltas [B][n][4] per level; i0..5 B,nlevels,(unused),A,topk,kmax; i6..10 n per level;
 //                  f0..3 img_h,img_w,min_size,score_thresh; d0 iou
 //   ROI_ALIGN      p0..3 feats; p4 rois; p5 counts; p6 out; i0..10 mode,R,RMAX,B,C,PH,PW,sr,nlevels,
 //                  k_min,k_max; i11..14 H; i15..18 W; f0..3 scales
@@ -31,6 +31,7 @@
 //                  f0,f1 img_h,img_w
 //   BOX_CLASS_NMS  p0 scores; p1 boxes; p2 counts; p3..7 records; i0..3 B,R,NC,kmax;
 //                  f0 score_thresh; f1 min_size; d0 iou
+//   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 #include <mutex>
 #include <string>
 
@@ -138,7 +139,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             return channel_mean_launch(P<const float>(o, 0), P<float>(o, 1), (int)I[0], (int)I[1], (int)I[2], s);
         case EDGEDET_OP_SE_FC:
             return se_fc_launch(P<const float>(o, 0), P<const float>(o, 1), P<const float>(o, 2), P<const float>(o, 3),
-                                P<const float>(o, 4), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2], s);
+                                P<const float>(o, 4), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2], (int)I[3], s);
         case EDGEDET_OP_MAXPOOL: {
             PoolParams p{};
             p.x = P<const float>(o, 0);
@@ -186,7 +187,8 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.topk = (int)I[4];
             EDGEDET_REQUIRE(p.nlevels >= 1 && p.nlevels <= 5, "rpn: 1..5 levels");
             for (int l = 0; l < p.nlevels; ++l) {
-                p.lv[l].head = P<const float>(o, l);
+                p.lv[l].obj = P<const float>(o, l);
+                p.lv[l].deltas = P<const float>(o, 15 + l);
                 p.lv[l].anchors = P<const float>(o, 5 + l);
                 p.lv[l].n = (int)I[6 + l];
             }
@@ -194,7 +196,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.img_w = o.f[1];
             p.min_size = o.f[2];
             p.score_thresh = o.f[3];
-            p.iou = o.d[0];
+            p.iou = make_iou_thr(o.d[0]);
             return rpn_level_nms_launch(p, seg_out(o, 10, (int)I[5]), s);
         }
         case EDGEDET_OP_ROI_ALIGN: {
@@ -234,14 +236,63 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
     }
 }
 
+// Side streams and fork/join events, created once per (thread, device) and reused by every call.
+struct Lanes {
+    int device = -1;
+    hipStream_t side[EDGEDET_MAX_LANES] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[EDGEDET_MAX_LANES] = {};
+};
+static thread_local Lanes g_lanes;
+
+static int lanes_ready() {
+    int dev = 0;
+    EDGEDET_CHECK_HIP(hipGetDevice(&dev));
+    if (g_lanes.device == dev) return 0;
+    g_lanes = Lanes();
+    for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
+        EDGEDET_CHECK_HIP(hipStreamCreateWithFlags(&g_lanes.side[l], hipStreamNonBlocking));
+        EDGEDET_CHECK_HIP(hipEventCreateWithFlags(&g_lanes.join_ev[l], hipEventDisableTiming));
+    }
+    EDGEDET_CHECK_HIP(hipEventCreateWithFlags(&g_lanes.fork_ev, hipEventDisableTiming));
+    g_lanes.device = dev;
+    return 0;
+}
+
 static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
+    bool need_lanes = false;
+    for (int64_t k = 0; k < n && !need_lanes; ++k)
+        need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
+    if (need_lanes && lanes_ready() != 0) return -2;
+    int forked = 0;
     for (int64_t k = 0; k < n; ++k) {
-        const int rc = run_op(ops[k], s);
+        const edgedet_op& o = ops[k];
+        int rc = 0;
+        if (o.kind == EDGEDET_OP_FORK) {
+            forked = (int)o.i[0];
+            EDGEDET_REQUIRE(forked >= 1 && forked < EDGEDET_MAX_LANES, "fork: 1..3 side lanes");
+            EDGEDET_CHECK_HIP(hipEventRecord(g_lanes.fork_ev, s));
+            for (int l = 1; l <= forked; ++l) EDGEDET_CHECK_HIP(hipStreamWaitEvent(g_lanes.side[l], g_lanes.fork_ev, 0));
+        } else if (o.kind == EDGEDET_OP_JOIN) {
+            const int nl = (int)o.i[0];
+            EDGEDET_REQUIRE(nl >= 1 && nl < EDGEDET_MAX_LANES, "join: 1..3 side lanes");
+            for (int l = 1; l <= nl; ++l) {
+                EDGEDET_CHECK_HIP(hipEventRecord(g_lanes.join_ev[l], g_lanes.side[l]));
+                EDGEDET_CHECK_HIP(hipStreamWaitEvent(s, g_lanes.join_ev[l], 0));
+            }
+            forked = 0;
+        } else {
+            const int lane = (int)o.i[EDGEDET_OP_LANE];
+            EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
+                            "op on a lane that is not forked");
+            rc = run_op(o, lane == 0 ? s : g_lanes.side[lane]);
+        }
         if (rc != 0) {
-            set_error("op " + std::to_string(k) + " (kind " + std::to_string(ops[k].kind) + "): " + g_error);
+            set_error("op " + std::to_string(k) + " (kind " + std::to_string(o.kind) + "): " + g_error);
             return rc;
         }
     }
+    EDGEDET_REQUIRE(forked == 0, "plan ends with side lanes still forked (missing JOIN)");
     return 0;
 }
 

@@ -17,6 +17,7 @@ struct ConvParams {
     int64_t x_bstride, y_bstride, res_bstride, y_off;
     int res_H, res_W;
     float res_sh, res_sw;  // nearest-upsample scales (in/out) for the residual
+    int lin_x, lin_y, lin_res;  // dense-layout fast paths (set by conv_launch)
     FastDiv div_howo, div_wo, div_cin, div_kw;
 };
 
@@ -65,16 +66,25 @@ struct SegOut {
 };
 
 struct RpnLevel {
-    const float* head;     // [B][HW][ld]: objectness at [a], deltas at [A + 4a + 0..3]
+    const float* obj;      // [B][HW*A] objectness logits (dense, anchor order (y, x, a))
+    const float* deltas;   // [B][HW*A][4] box deltas
     const float* anchors;  // [HW*A][4]
     int n;                 // HW*A
 };
+
+// NMS IoU threshold in exact-comparison form (detect.hip iou_gt).
+struct IouThr {
+    double thr;  // the reference's double threshold
+    double mid;  // midpoint of the float pair (t0, t1) around thr, t1 = smallest float > thr
+    int tie_up;  // round-half-even of a tie at mid goes to t1
+};
+IouThr make_iou_thr(double thr);
 
 struct RpnParams {
     RpnLevel lv[5];
     int nlevels, ld, A, B, topk;
     float img_h, img_w, min_size, score_thresh;
-    double iou;
+    IouThr iou;
 };
 
 struct MergeParams {
@@ -95,8 +105,9 @@ int conv_launch(ConvParams p, int tile, hipStream_t s);
 int preprocess_launch(const PreParams& p, hipStream_t s);
 int dwconv_launch(const DwParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);
-int se_fc_launch(const float* mean, const float* w1t, const float* b1, const float* w2t, const float* b2,
-                 float* scale, int B, int C, int S, hipStream_t s);
+int se_fc_launch(const float* mean, const float* w1, const float* b1, const float* w2t, const float* b2,
+                 float* scale, int B, int C, int S, int HW, hipStream_t s);
+constexpr int SE_PARTS = 16;  // pixel splits of the SE squeeze (layers.hip SE_SPLITS)
 int maxpool_launch(const PoolParams& p, hipStream_t s);
 int roi_align_launch(const RoiParams& p, hipStream_t s);
 int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,

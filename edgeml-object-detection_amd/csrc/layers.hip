@@ -109,60 +109,91 @@ int dwconv_launch(const DwParams& p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------ SE squeeze
-// grid (cdiv(C, 64), B), block 256 = 64 channels x 4 pixel groups.
-__global__ void channel_mean_kernel(const float* __restrict__ x, float* __restrict__ out, int HW, int C) {
-    __shared__ float part[4][64];
-    const int b = blockIdx.y;
+// Partial channel sums: grid (cdiv(C, 64), B, S) with block 256 = 64 channels x 4 pixel groups; split s
+// covers pixels [s*HW/S, (s+1)*HW/S).  part[b][s][c] is reduced in fixed order by se_fc_kernel
+// (deterministic, no atomics).
+
+__global__ void channel_sum_kernel(const float* __restrict__ x, float* __restrict__ part, int HW, int C, int S) {
+    __shared__ float red[4][64];
+    const int b = blockIdx.y, sidx = blockIdx.z;
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
-    float s = 0.f;
+    const int p0 = (int)((int64_t)sidx * HW / S), p1 = (int)((int64_t)(sidx + 1) * HW / S);
+    float acc = 0.f;
     if (c < C) {
         const float* xb = x + (int64_t)b * HW * C + c;
-        for (int i = g; i < HW; i += 4) s += xb[(int64_t)i * C];
+        for (int i = p0 + g; i < p1; i += 4) acc += xb[(int64_t)i * C];
     }
-    part[g][cl] = s;
+    red[g][cl] = acc;
     __syncthreads();
-    if (g == 0 && c < C) out[(int64_t)b * C + c] = (((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl]) / (float)HW;
+    if (g == 0 && c < C)
+        part[((int64_t)b * S + sidx) * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s) {
     EDGEDET_REQUIRE(x && out, "channel_mean: null pointer");
-    hipLaunchKernelGGL(channel_mean_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), 0, s, x, out, HW, C);
+    hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)cdiv(C, 64), B, SE_PARTS), dim3(256), 0, s, x, out, HW, C,
+                       SE_PARTS);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
 
 // ------------------------------------------------------------------------------ SE excitation
-// One block per image.  w1t [C][S] (fc1 transposed), w2t [S][C] (fc2 transposed).
-__global__ void se_fc_kernel(const float* __restrict__ mean, const float* __restrict__ w1t,
-                             const float* __restrict__ b1, const float* __restrict__ w2t,
-                             const float* __restrict__ b2, float* __restrict__ scale, int C, int S) {
+// grid (cdiv(C, 64), B): every block recomputes the (small) fc1 of its image from the partial sums
+// part [B][SE_PARTS][C] (mean = sum / HW, fixed reduction order), then evaluates fc2 + Hardsigmoid
+// for its 64 channels.  w1 [S][C] (fc1 as stored), w2t [S][C] (fc2 transposed).  fc1 splits the C
+// reduction over the 64 lanes of a wave; fc2 splits the S reduction over 4 waves.
+__global__ void __launch_bounds__(256) se_fc_kernel(const float* __restrict__ part, const float* __restrict__ w1,
+                                                    const float* __restrict__ b1, const float* __restrict__ w2t,
+                                                    const float* __restrict__ b2, float* __restrict__ scale, int C,
+                                                    int S, int HW) {
     extern __shared__ float sm[];
-    float* m = sm;      // [C]
-    float* s1 = sm + C; // [S]
-    const int b = blockIdx.x;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) m[c] = mean[(int64_t)b * C + c];
-    __syncthreads();
-    for (int j = threadIdx.x; j < S; j += blockDim.x) {
-        float a = 0.f;
-        for (int c = 0; c < C; ++c) a = fmaf(w1t[(int64_t)c * S + j], m[c], a);
-        a += b1[j];
-        s1[j] = a > 0.f ? a : 0.f;
+    float* m = sm;             // [C]
+    float* s1 = sm + C;        // [S]
+    float* red = s1 + S;       // [256]
+    const int b = blockIdx.y;
+    const int tid = threadIdx.x;
+    for (int c = tid; c < C; c += 256) {
+        float acc = 0.f;
+        for (int k = 0; k < SE_PARTS; ++k) acc += part[((int64_t)b * SE_PARTS + k) * C + c];
+        m[c] = acc / (float)HW;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    // fc1: wave w owns outputs j = w, w+4, ...; its 64 lanes split the C reduction (fixed order:
+    // lane-strided partial sums, then a butterfly)
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int j = wv; j < S; j += 4) {
         float a = 0.f;
-        for (int j = 0; j < S; ++j) a = fmaf(w2t[(int64_t)j * C + c], s1[j], a);
-        scale[(int64_t)b * C + c] = apply_act(a + b2[c], ACT_HSIGMOID);
+        for (int c = lane; c < C; c += 64) a = fmaf(w1[(int64_t)j * C + c], m[c], a);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        if (lane == 0) {
+            a += b1[j];
+            s1[j] = a > 0.f ? a : 0.f;
+        }
+    }
+    __syncthreads();
+    const int cl = tid & 63, g = tid >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    float a = 0.f;
+    if (c < C)
+        for (int j = g; j < S; j += 4) a = fmaf(w2t[(int64_t)j * C + c], s1[j], a);
+    red[tid] = a;
+    __syncthreads();
+    if (g == 0 && c < C) {
+        const float v = ((red[cl] + red[64 + cl]) + red[128 + cl]) + red[192 + cl];
+        scale[(int64_t)b * C + c] = apply_act(v + b2[c], ACT_HSIGMOID);
     }
 }
 
-int se_fc_launch(const float* mean, const float* w1t, const float* b1, const float* w2t, const float* b2,
-                 float* scale, int B, int C, int S, hipStream_t s) {
-    EDGEDET_REQUIRE(mean && w1t && b1 && w2t && b2 && scale, "se_fc: null pointer");
-    const size_t lds = (size_t)(C + S) * sizeof(float);
+int se_fc_launch(const float* mean, const float* w1, const float* b1, const float* w2t, const float* b2,
+                 float* scale, int B, int C, int S, int HW, hipStream_t s) {
+    EDGEDET_REQUIRE(mean && w1 && b1 && w2t && b2 && scale, "se_fc: null pointer");
+    EDGEDET_REQUIRE(S >= 1 && S <= 256, "se_fc: squeeze width must be in [1, 256]");
+    const size_t lds = (size_t)(C + S + 256) * sizeof(float);
     EDGEDET_REQUIRE(lds <= 60 * 1024, "se_fc: too many channels");
-    hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), lds, s, mean, w1t, b1, w2t, b2, scale, C, S);
+    hipLaunchKernelGGL(se_fc_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), lds, s, mean, w1, b1, w2t, b2, scale,
+                       C, S, HW);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

@@ -179,7 +179,7 @@ class SSDLite320(_Detector):
         if key not in self._w:
             w1 = _np(self.sd[p + ".fc1.weight"])[:, :, 0, 0]  # [S, C]
             w2 = _np(self.sd[p + ".fc2.weight"])[:, :, 0, 0]  # [C, S]
-            self._w[key] = (self.pack.add(w1.T), self.pack.add(_np(self.sd[p + ".fc1.bias"])),
+            self._w[key] = (self.pack.add(w1), self.pack.add(_np(self.sd[p + ".fc1.bias"])),
                             self.pack.add(w2.T), self.pack.add(_np(self.sd[p + ".fc2.bias"])), w1.shape[0])
         return self._w[key]
 
@@ -219,12 +219,13 @@ class SSDLite320(_Detector):
 
         def se(cur, p):
             xb, xs = cur
-            w1t, b1, w2t, b2, sq = self._se(p)
+            w1, b1, w2t, b2, sq = self._se(p)
             C = xs[3]
-            mean = P.buf((B, C), name=p + ".mean")
+            part = P.buf((B, ops.SE_PARTS, C), name=p + ".partial_sums")
             scale = P.buf((B, C), name=p + ".scale")
-            P.add(Op(ops.CHANNEL_MEAN, {0: B, 1: xs[1] * xs[2], 2: C}, {0: xb, 1: mean}, name=p + ".avgpool"))
-            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq}, {0: mean, 1: w1t, 2: b1, 3: w2t, 4: b2, 5: scale}, name=p))
+            HW = xs[1] * xs[2]
+            P.add(Op(ops.CHANNEL_MEAN, {0: B, 1: HW, 2: C}, {0: xb, 1: part}, name=p + ".avgpool"))
+            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: HW}, {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale}, name=p))
             return scale
 
         def inverted_residual(cur, cnf, base):
@@ -264,16 +265,22 @@ class SSDLite320(_Detector):
         cls = P.buf((B, A, NC), name="cls_logits")
         reg = P.buf((B, A, 4), name="bbox_regression")
         off = 0
+        # the 12 head branches are independent: spread them over 4 stream lanes
+        P.fork(3)
+        chain = 0
         for i, f in enumerate(feats):
             fb, fs = f
             for name, cols, out in (("classification_head", NC, cls), ("regression_head", 4, reg)):
                 p = f"head.{name}.module_list.{i}"
+                P.lane(chain % 4)
+                chain += 1
                 t = dw(f, p + ".0", 3, 1, "R6")
                 w, b, K, Kpad, cin = self._conv_bias(p + ".1.weight", p + ".1.bias")
                 cout = 6 * cols
                 conv_op(P, t[0], t[1], w, b, cout, 1, 1, 0, None, out, (B, fs[1], fs[2], cout), K, Kpad,
                         y_pstride=cout, y_bstride=A * cols, y_off=off * cols, name=p + ".1")
             off += fs[1] * fs[2] * 6
+        P.join()
         self.grids = grids
         if pack_only:
             return P
@@ -345,15 +352,6 @@ class FasterRCNNFPNv2(_Detector):
             self._w[key] = (self.pack.add(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
         return self._w[key]
 
-    def _rpn_out(self):
-        key = ("rpn_out",)
-        if key not in self._w:
-            p = "rpn.head."
-            w = np.concatenate([_np(self.sd[p + "cls_logits.weight"]), _np(self.sd[p + "bbox_pred.weight"])], 0)
-            b = np.concatenate([_np(self.sd[p + "cls_logits.bias"]), _np(self.sd[p + "bbox_pred.bias"])], 0)
-            wp, K, Kpad, cin = pack_conv_weight(w.astype(np.float32))
-            self._w[key] = (self.pack.add(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
-        return self._w[key]
 
     def resized_size(self, H, W):
         scale = min(float(self.MIN_SIZE) / min(H, W), float(self.MAX_SIZE) / max(H, W))
@@ -427,9 +425,8 @@ class FasterRCNNFPNv2(_Detector):
             outs.insert(0, conv(last, f"{f}layer_blocks.{i}.0.weight", f"{f}layer_blocks.{i}.1", 3, 1, None))
         outs.append(maxpool(outs[-1], 1, 2, 0, "backbone.fpn.extra_blocks.pool"))
         if pack_only:
-            for k in ("rpn.head.conv.0.0", "rpn.head.conv.1.0"):
+            for k in ("rpn.head.conv.0.0", "rpn.head.conv.1.0", "rpn.head.cls_logits", "rpn.head.bbox_pred"):
                 self._conv_bias(k + ".weight", k + ".bias")
-            self._rpn_out()
             for i in range(4):
                 self._conv_bn(f"roi_heads.box_head.{i}.0.weight", f"roi_heads.box_head.{i}.1", self.BN_EPS)
             self._fc6()
@@ -439,28 +436,33 @@ class FasterRCNNFPNv2(_Detector):
         # ---- RPN head (shared over levels) + proposal filtering
         A = 3
         heads, grids = [], []
+        P.fork(3)  # the five RPN head levels are independent
         for lvl, fm in enumerate(outs):
+            P.lane(lvl % 4)
             t = conv(fm, "rpn.head.conv.0.0.weight", None, 3, 1, "RE", bias_key="rpn.head.conv.0.0.bias",
                      name=f"rpn.head.conv.0@{lvl}")
             t = conv(t, "rpn.head.conv.1.0.weight", None, 3, 1, "RE", bias_key="rpn.head.conv.1.0.bias",
                      name=f"rpn.head.conv.1@{lvl}")
-            w, b, K, Kpad, cin = self._rpn_out()
-            hs = (B, fm[1][1], fm[1][2], 15)
-            hb = P.buf(hs, name=f"rpn.head.out@{lvl}")
-            conv_op(P, t[0], t[1], w, b, 15, 1, 1, 0, None, hb, hs, K, Kpad, name=f"rpn.head.cls_bbox@{lvl}")
-            heads.append(hb)
+            # objectness [B, HW*A] (dense: the top-k reads it contiguously) and deltas [B, HW*A, 4]
+            o = conv(t, "rpn.head.cls_logits.weight", None, 1, 1, None, bias_key="rpn.head.cls_logits.bias",
+                     name=f"rpn.head.cls_logits@{lvl}")
+            d = conv(t, "rpn.head.bbox_pred.weight", None, 1, 1, None, bias_key="rpn.head.bbox_pred.bias",
+                     name=f"rpn.head.bbox_pred@{lvl}")
+            heads.append((o[0], d[0]))
             grids.append((fm[1][1], fm[1][2]))
+        P.join()
         anchor_bufs = [P.const(a, name=f"rpn.anchors@{l}") for l, a in enumerate(anc.rpn_anchors(grids, (Hp, Wp)))]
         L = len(outs)
         KM = self.RPN_PRE
         rrec = [P.buf((B, L, KM, 4), name="rpn.rec.box"), P.buf((B, L, KM), name="rpn.rec.score"),
                 P.buf((B, L, KM), torch.int32, name="rpn.rec.tb"), P.buf((B, L, KM), torch.int32, name="rpn.rec.lvl"),
                 P.buf((B, L), torch.int32, name="rpn.rec.count")]
-        pi = {0: B, 1: L, 2: 15, 3: A, 4: self.RPN_PRE, 5: KM}
+        pi = {0: B, 1: L, 2: 0, 3: A, 4: self.RPN_PRE, 5: KM}
         pp = {}
         for l in range(L):
             pi[6 + l] = grids[l][0] * grids[l][1] * A
-            pp[l] = heads[l]
+            pp[l] = heads[l][0]
+            pp[15 + l] = heads[l][1]
             pp[5 + l] = anchor_bufs[l]
         for j in range(5):
             pp[10 + j] = rrec[j]

@@ -19,6 +19,10 @@ OP_INTS, OP_PTRS, OP_DBLS, OP_FLTS = 48, 24, 8, 16
 # kinds (include/edgedet.h)
 MEMSET, PREPROCESS, CONV, DWCONV, CHANNEL_MEAN, SE_FC, MAXPOOL = 1, 2, 3, 4, 5, 6, 7
 SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX_CLASS_NMS = 8, 9, 10, 11, 12, 13, 14
+FORK, JOIN = 15, 16
+LANE_FIELD, MAX_LANES = 47, 4
+
+SE_PARTS = 16  # pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
 
 # activations (csrc/common.hpp)
 ACT = {None: 0, "RE": 1, "R6": 2, "HS": 3, "HSIG": 4, "SIG": 5}
@@ -127,15 +131,31 @@ def roi_align_nhwc(feat_nhwc, rois, spatial_scale, output_size=7, sampling_ratio
     return out
 
 
-def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None):
-    """Fused conv (+ folded BN) + residual + activation on NHWC; w_packed from pack_conv_weight."""
-    _need_cuda(x, w_packed, bias, res)
+def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, tile=0, in_scale=None):
+    """Fused conv (+ folded BN) + residual + activation on NHWC; w_packed from plan.pack_conv_weight.
+
+    tile=0 goes through the C entry point edgedet_conv2d (automatic tile choice); a non-zero tile
+    (or an SE ``in_scale`` [B, Cin]) runs one CONV plan record so every kernel variant is testable.
+    """
+    _need_cuda(x, w_packed, bias, res, in_scale)
     B, H, W, Cin = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
-    check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad, ACT[act],
-                               _ptr(res), _ptr(y), stream_handle()))
+    if tile == 0 and in_scale is None:
+        check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad,
+                                   ACT[act], _ptr(res), _ptr(y), stream_handle()))
+        return y
+    K = k * k * Cin
+    kpad = int(lib().edgedet_conv_weight_k(k, k, Cin))
+    rec = np.zeros(1, dtype=OP_DTYPE)
+    rec[0]["kind"] = CONV
+    vals = [B, H, W, Cin, Ho, Wo, cout, k, k, stride, pad, ACT[act], K, kpad, Cin, cout, cout, H * W * Cin,
+            Ho * Wo * cout, Ho * Wo * cout, 0, Ho, Wo, tile]
+    rec[0]["i"][:len(vals)] = vals
+    for j, t in enumerate((x, w_packed, bias, y, res, in_scale)):
+        rec[0]["p"][j] = 0 if t is None else t.data_ptr()
+    check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
     return y
 
 

@@ -106,8 +106,8 @@ class Buf:
 
 
 class Op:
-    def __init__(self, kind, i=None, p=None, f=None, d=None, name=""):
-        self.kind, self.name = kind, name
+    def __init__(self, kind, i=None, p=None, f=None, d=None, name="", lane=0):
+        self.kind, self.name, self.lane = kind, name, lane
         self.i = dict(i or {})
         self.p = dict(p or {})
         self.f = dict(f or {})
@@ -141,8 +141,25 @@ class Plan:
         return b
 
     def add(self, op):
+        if op.lane == 0 and getattr(self, "_lane", 0):
+            op.lane = self._lane
         self.ops.append(op)
         return op
+
+    # concurrency ---------------------------------------------------------------------------
+    def fork(self, nlanes):
+        """Side lanes 1..nlanes start after everything issued so far (independent branches)."""
+        self.ops.append(Op(ops.FORK, {0: nlanes}, name="fork"))
+        self._forked = nlanes
+
+    def lane(self, k):
+        """Issue the following ops on lane k (0 = the caller's stream)."""
+        self._lane = k
+
+    def join(self):
+        self._lane = 0
+        self.ops.append(Op(ops.JOIN, {0: self._forked}, name="join"))
+        self._forked = 0
 
     # finalizing ---------------------------------------------------------------------------
     def finalize(self):
@@ -159,6 +176,7 @@ class Plan:
             rec[k]["kind"] = op.kind
             for j, v in op.i.items():
                 rec[k]["i"][j] = int(v)
+            rec[k]["i"][ops.LANE_FIELD] = op.lane
             for j, v in op.p.items():
                 if v is None:
                     rec[k]["p"][j] = 0

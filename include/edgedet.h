@@ -60,8 +60,16 @@ enum {
     EDGEDET_OP_RPN_LEVEL_NMS = 11,/* per (image, FPN level): top-k logits, decode, clip, small, NMS   */
     EDGEDET_OP_ROI_ALIGN = 12,    /* MultiScaleRoIAlign (LevelMapper + roi_align 7x7, sr=2)          */
     EDGEDET_OP_BOX_SCORES = 13,   /* RoIHeads softmax + class-specific decode + clip                 */
-    EDGEDET_OP_BOX_CLASS_NMS = 14 /* per (image, class): score>t, remove_small, NMS                   */
+    EDGEDET_OP_BOX_CLASS_NMS = 14,/* per (image, class): score>t, remove_small, NMS                   */
+    EDGEDET_OP_FORK = 15,         /* side lanes 1..i[0] wait for everything issued so far on lane 0    */
+    EDGEDET_OP_JOIN = 16          /* lane 0 waits for everything issued so far on lanes 1..i[0]        */
 };
+
+/* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,
+ * 1..3 = side streams owned by the library (joined back by EDGEDET_OP_JOIN; captured graphs keep
+ * the fork/join as graph dependencies). */
+#define EDGEDET_OP_LANE 47
+#define EDGEDET_MAX_LANES 4
 
 /* Run ops[0..n) on `stream`.  Shapes are checked on the host before any launch. */
 int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream);

@@ -18,7 +18,7 @@ def _act(y, act):
     return {None: y, "RE": F.relu(y), "R6": F.relu6(y), "HS": F.hardswish(y)}[act]
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,act,res", [
+CONV_CASES = [
     (2, 17, 19, 4, 16, 3, 2, "HS", False),      # SSD stem shape class (Cin padded to 4)
     (2, 20, 20, 112, 672, 1, 1, "HS", False),   # expansion 1x1
     (3, 10, 10, 480, 80, 1, 1, None, True),     # projection with residual
@@ -27,26 +27,53 @@ def _act(y, act):
     (1, 40, 36, 4, 64, 7, 2, "RE", False),      # ResNet stem 7x7 (Cin padded to 4)
     (2, 7, 7, 256, 24, 1, 1, None, False),      # narrow Cout
     (4, 1, 1, 1024, 455, 1, 1, None, False),    # FC as 1x1 (predictor shape)
-])
-def test_conv_matches_torch(B, H, W, Cin, Cout, k, s, act, res):
+    (2, 33, 31, 24, 72, 1, 1, "RE", False),     # K=24 (one partial K stage)
+    (1, 9, 9, 16, 16, 1, 1, None, True),        # K=16 with residual
+]
+
+
+def _conv_case(B, H, W, Cin, Cout, k, s, act, res, tile=0, se=False):
     from edgeml_amd import ops
     from edgeml_amd.plan import pack_conv_weight
     g = torch.Generator().manual_seed(1)
     x = torch.randn(B, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
     b = torch.randn(Cout, generator=g) * 0.1
+    sc = torch.rand(B, Cin, generator=g) if se else None
     pad = (k - 1) // 2
-    ref = F.conv2d(x, w, b, s, pad)
+    xin = x * sc[:, :, None, None] if se else x
+    ref = F.conv2d(xin, w, b, s, pad)
     r = torch.randn_like(ref) if res else None
     if res:
         ref = ref + r
     ref = _act(ref, act)
     wp, K, Kpad, _ = pack_conv_weight(w.numpy())
     out = ops.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(wp).to(DEV), b.to(DEV), Cout,
-                          k, s, pad, act, r.permute(0, 2, 3, 1).contiguous().to(DEV) if res else None)
+                          k, s, pad, act, r.permute(0, 2, 3, 1).contiguous().to(DEV) if res else None, tile=tile,
+                          in_scale=sc.to(DEV) if se else None)
     got = out.permute(0, 3, 1, 2).cpu()
     err = (got - ref).abs().max().item()
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_matches_torch(case):
+    _conv_case(*case)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (1, 2, 4, 5, 8)])
+def test_conv_every_lds_tile(case, tile):
+    _conv_case(*case, tile=tile)
+
+
+@pytest.mark.parametrize("tile", [10, 11, 12])
+@pytest.mark.parametrize("case", [(2, 20, 20, 112, 672, 1, 1, "HS", False), (3, 10, 10, 40, 120, 1, 1, None, True),
+                                  (2, 33, 31, 24, 72, 1, 1, "RE", False), (1, 9, 9, 16, 16, 1, 1, None, True),
+                                  (2, 13, 11, 96, 24, 1, 1, "R6", False)])
+@pytest.mark.parametrize("se", [False, True])
+def test_conv_direct_pointwise(case, tile, se):
+    _conv_case(*case, tile=tile, se=se)
 
 
 @pytest.mark.parametrize("B,H,W,C,k,s,act", [(2, 20, 20, 72, 5, 2, "RE"), (3, 10, 10, 672, 5, 1, "HS"),
@@ -114,3 +141,20 @@ def test_roi_align_matches_oracle():
     got = ops.roi_align_nhwc(feat.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(rois).to(DEV), 0.25)
     got = got.permute(0, 3, 1, 2).cpu()
     assert torch.equal(got, ref), (got - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("thr", [0.5, 0.55, 0.7, 0.3, 1.0 / 3.0])
+def test_nms_exact_ratio_boundaries(thr):
+    """Integer-coordinate boxes make IoUs hit exact ratios (1/2, 7/10, 11/20, ...) on the threshold:
+    the engine's division-free IoU test must decide exactly like the reference's float division."""
+    from edgeml_amd import ops
+    from oracle import tv_ops
+    rs = np.random.RandomState(int(thr * 1000))
+    n = 600
+    xy = rs.randint(0, 12, (n, 2)).astype(np.float32)
+    wh = rs.randint(1, 10, (n, 2)).astype(np.float32)
+    boxes = np.concatenate([xy, xy + wh], 1).astype(np.float32)
+    scores = rs.permutation(n).astype(np.float32) / n
+    ref = tv_ops.nms(boxes, scores, thr)
+    got = ops.nms(torch.from_numpy(boxes).to(DEV), torch.from_numpy(scores).to(DEV), thr).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)

@@ -142,6 +142,9 @@ def test_ssd_plan_lowering():
     P = m.build_plan(4, 640, 480)
     kinds = [op.kind for op in P.ops]
     assert kinds[0] == ops.PREPROCESS and kinds[-1] == ops.MERGE_TOPK
+    assert kinds.count(ops.FORK) == kinds.count(ops.JOIN) == 1
+    lanes = {op.lane for op in P.ops}
+    assert lanes == {0, 1, 2, 3}
     # convs: stem 1 + blocks 0-11 (block 0 has no expansion: 1 + 11*2) + C4 split 2 + blocks 13-14 (2*2)
     #        + last 1 + extras 4*2 + head 6*2
     n_conv = kinds.count(ops.CONV)
@@ -164,4 +167,4 @@ def test_frcnn_plan_lowering():
     assert pre.i[5] == 800 and pre.i[6] == 1088  # padded to /32
     kinds = [op.kind for op in P.ops]
     assert kinds.count(ops.ROI_ALIGN) == 1 and kinds.count(ops.RPN_LEVEL_NMS) == 1
-    assert kinds.count(ops.CONV) == 1 + 16 * 3 + 4 + 8 + 5 * 3 + 4 + 2
+    assert kinds.count(ops.CONV) == 1 + 16 * 3 + 4 + 8 + 5 * 4 + 4 + 2
