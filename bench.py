@@ -99,7 +99,7 @@ def op_work(op):
     if k == O.CHANNEL_MEAN:
         return "se_squeeze", float(i[0] * i[1] * i[2]), 4.0 * i[0] * i[1] * i[2]
     if k == O.SE_FC:
-        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * (2 * i[1] * i[2] + i[0] * O.SE_PARTS * i[1])
+        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * (2 * i[1] * i[2] + i[0] * (O.SE_PARTS + 1) * i[1] + 2 * i[0] * i[2])
     if k == O.MAXPOOL:
         B, H, W, C, Ho, Wo = (i[j] for j in range(6))
         return "maxpool", 0.0, 4.0 * (B * H * W * C + B * Ho * Wo * C)
@@ -109,6 +109,9 @@ def op_work(op):
     if k == O.SSD_CLASS_NMS:
         B, A, NC = i[0], i[1], i[2]
         return "class_nms", 0.0, 4.0 * (B * NC * A + B * A * 4)
+    if k == O.SSD_POSTPROCESS:
+        B, A, NC, KM = i[0], i[1], i[2], i[3]
+        return "ssd_nms", 0.0, 4.0 * (B * NC * A + B * A * 4 + 2 * 2 * B * (NC - 1) * KM)
     if k == O.MERGE_TOPK:
         return "merge_topk", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
     if k == O.RPN_LEVEL_NMS:

@@ -173,6 +173,29 @@ struct BlockScan {
         total = tot;
         return base + in_wave;
     }
+    // exclusive prefix of an integer per thread (thread order); *total = block sum.
+    __device__ static int exclusive_sum(int v, int* wsum, int& total) {
+        constexpr int NW = NT / 64;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        int inc = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(inc, off);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        int base = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int x = wsum[i];
+            base += (i < w) ? x : 0;
+            tot += x;
+        }
+        __syncthreads();
+        total = tot;
+        return base + inc - v;
+    }
 };
 
 // LDS layout of a segment kernel with capacity KC (power of two, >= 64).
@@ -196,6 +219,31 @@ __device__ __forceinline__ int key_index(unsigned long long key) {
     return (int)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
 }
 
+// Keys are produced by fkey(i, k) -> valid.  Every pass below evaluates U keys per thread before
+// using any of them (indices clamped, loads unconditional and pinned with an empty asm so the
+// compiler cannot sink them back under the bounds test): U memory round trips overlap instead of
+// one dependent round trip per element.
+constexpr int KEY_U = 8;
+
+template <int NT, typename F, typename G>
+__device__ __forceinline__ void for_keys(int n, F fkey, G body) {
+    for (int base = 0; base < n; base += NT * KEY_U) {
+        uint32_t k[KEY_U];
+        bool v[KEY_U];
+#pragma unroll
+        for (int u = 0; u < KEY_U; ++u) {
+            const int i = base + u * NT + (int)threadIdx.x;
+            v[u] = fkey(i < n ? i : n - 1, k[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < KEY_U; ++u) {
+            asm volatile("" : "+v"(k[u]));
+            const int i = base + u * NT + (int)threadIdx.x;
+            body(v[u] & (i < n), k[u]);
+        }
+    }
+}
+
 // Block radix select: T = the K-th largest key among candidates with fkey(i, k) == true.
 // misc[1] = number of valid candidates, misc[5] = how many keys == T belong to the top K.
 // If valid <= K, returns 0 and misc[5] = 0 (take every valid candidate).
@@ -204,10 +252,7 @@ __device__ uint32_t radix_select(int n, int K, F fkey, unsigned int* hist, int* 
     if (threadIdx.x == 0) misc[0] = 0;
     __syncthreads();
     int cnt = 0;
-    for (int i = threadIdx.x; i < n; i += NT) {
-        uint32_t k;
-        if (fkey(i, k)) ++cnt;
-    }
+    for_keys<NT>(n, fkey, [&](bool v, uint32_t) { cnt += v ? 1 : 0; });
     atomicAdd(&misc[0], cnt);
     __syncthreads();
     const int nvalid = misc[0];
@@ -225,10 +270,9 @@ __device__ uint32_t radix_select(int n, int K, F fkey, unsigned int* hist, int* 
     for (int shift = 24; shift >= 0; shift -= 8) {
         for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0;
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += NT) {
-            uint32_t k;
-            if (fkey(i, k) && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
-        }
+        for_keys<NT>(n, fkey, [&](bool v, uint32_t k) {
+            if (v && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        });
         __syncthreads();
         if (threadIdx.x == 0) {
             int acc = 0, d = 255;
@@ -318,28 +362,47 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
 }
 
 // Ordered compaction into keys[]: every valid key > T (all valid when take_all) plus the first
-// `eq_budget` keys == T in index order; at most `cap` written.  Returns the count.
+// `eq_budget` keys == T in index order; at most `cap` written.  Returns the count.  Each batch
+// gives thread t the KEY_U consecutive indices base + t*KEY_U + u (loads issued together), so one
+// block scan of per-thread counts orders the batch.
 template <int NT, typename F>
 __device__ int compact(int n, uint32_t T, bool take_all, int eq_budget, int cap, F fkey, unsigned long long* keys,
                        int* wsum) {
     int written = 0, eq_taken = 0;
-    for (int base = 0; base < n; base += NT) {
-        const int i = base + threadIdx.x;
-        uint32_t k = 0;
-        const bool v = (i < n) && fkey(i, k);
-        const bool gt = v && (take_all || k > T);
-        const bool eq = v && !take_all && k == T;
-        int tot_gt, tot_eq;
-        const int pos_gt = BlockScan<NT>::exclusive(gt ? 1 : 0, wsum, tot_gt);
-        const int pos_eq = BlockScan<NT>::exclusive(eq ? 1 : 0, wsum, tot_eq);
-        const int budget = eq_budget - eq_taken;
-        if (gt) {
-            const int slot = written + pos_gt;
-            if (slot < cap) keys[slot] = make_key(k, (uint32_t)i);
+    for (int base = 0; base < n; base += NT * KEY_U) {
+        uint32_t k[KEY_U];
+        bool v[KEY_U];
+#pragma unroll
+        for (int u = 0; u < KEY_U; ++u) {
+            const int i = base + (int)threadIdx.x * KEY_U + u;
+            v[u] = fkey(i < n ? i : n - 1, k[u]);
         }
-        if (eq && pos_eq < budget) {
-            const int slot = written + tot_gt + pos_eq;
-            if (slot < cap) keys[slot] = make_key(k, (uint32_t)i);
+        int ngt = 0, neq = 0;
+#pragma unroll
+        for (int u = 0; u < KEY_U; ++u) {
+            asm volatile("" : "+v"(k[u]));
+            const int i = base + (int)threadIdx.x * KEY_U + u;
+            v[u] = v[u] & (i < n);
+            ngt += (v[u] && (take_all || k[u] > T)) ? 1 : 0;
+            neq += (v[u] && !take_all && k[u] == T) ? 1 : 0;
+        }
+        int tot_gt, tot_eq;
+        int pos_gt = BlockScan<NT>::exclusive_sum(ngt, wsum, tot_gt);
+        int pos_eq = BlockScan<NT>::exclusive_sum(neq, wsum, tot_eq);
+        const int budget = eq_budget - eq_taken;
+#pragma unroll
+        for (int u = 0; u < KEY_U; ++u) {
+            const uint32_t i = (uint32_t)(base + (int)threadIdx.x * KEY_U + u);
+            if (v[u] && (take_all || k[u] > T)) {
+                const int slot = written + pos_gt++;
+                if (slot < cap) keys[slot] = make_key(k[u], i);
+            } else if (v[u] && !take_all && k[u] == T) {
+                if (pos_eq < budget) {
+                    const int slot = written + tot_gt + pos_eq;
+                    if (slot < cap) keys[slot] = make_key(k[u], i);
+                }
+                ++pos_eq;
+            }
         }
         const int eq_used = tot_eq < budget ? tot_eq : (budget > 0 ? budget : 0);
         written += tot_gt + eq_used;
@@ -506,28 +569,19 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int PER, int KC>
-__global__ void __launch_bounds__(256) ssd_class_nms_wave_kernel(const float* __restrict__ scores_t,
-                                                                 const f32x4* __restrict__ boxes, int A, int NC,
-                                                                 float score_thresh, int topk, IouThr iou,
-                                                                 SegOut out) {
-    constexpr int NQ = KC / 64;
-    __shared__ unsigned long long keys_s[4][KC];
-    __shared__ f32x4 box_s[4][KC];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 4 + w + 1;  // class 0 is background
-    const int b = blockIdx.y;
-    if (c >= NC) return;                   // whole wave leaves; nothing below waits on other waves
-    unsigned long long* keys = keys_s[w];
-    f32x4* bs = box_s[w];
+// Per-class candidate set of one wave: score > thresh, then the top-k by (score desc, index asc),
+// emitted in index order as emit(slot, key, anchor).  Returns the number emitted (<= topk).
+template <int PER, typename E>
+__device__ __forceinline__ int wave_select_topk(const float* __restrict__ sc, int A, float score_thresh, int topk,
+                                                E emit) {
+    const int lane = threadIdx.x & 63;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    const float* sc = scores_t + ((int64_t)b * NC + c) * A;
-
     uint32_t kr[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
+        // unconditional (clamped) loads: no branch between them, so all PER are in flight at once
         const int i = lane + 64 * j;
-        const float v = i < A ? sc[i] : 0.f;
+        const float v = sc[i < A ? i : A - 1];
         kr[j] = (i < A && v > score_thresh) ? __float_as_uint(v) : 0u;  // probabilities >= 0: bits ordered
     }
     auto count_ge = [&](uint32_t t) -> int {
@@ -559,20 +613,37 @@ __global__ void __launch_bounds__(256) ssd_class_nms_wave_kernel(const float* __
         const unsigned long long mg = __ballot(gt), me = __ballot(eq);
         const int ng = __popcll(mg), ne = __popcll(me);
         const int budget = need_eq - eq_taken;
-        const uint32_t i = (uint32_t)(lane + 64 * j);
-        if (gt) {
-            const int slot = written + __popcll(mg & lt_mask);
-            if (slot < KC) keys[slot] = make_key(k, i);
-        }
+        const int i = lane + 64 * j;
+        if (gt) emit(written + __popcll(mg & lt_mask), k, i);
         if (eq) {
             const int pe = __popcll(me & lt_mask);
-            const int slot = written + ng + pe;
-            if (pe < budget && slot < KC) keys[slot] = make_key(k, i);
+            if (pe < budget) emit(written + ng + pe, k, i);
         }
         const int used = ne < budget ? ne : (budget > 0 ? budget : 0);
         written += ng + used;
         eq_taken += used;
     }
+    return written;
+}
+
+template <int PER, int KC>
+__global__ void __launch_bounds__(256) ssd_class_nms_wave_kernel(const float* __restrict__ scores_t,
+                                                                 const f32x4* __restrict__ boxes, int A, int NC,
+                                                                 float score_thresh, int topk, IouThr iou,
+                                                                 SegOut out) {
+    constexpr int NQ = KC / 64;
+    __shared__ unsigned long long keys_s[4][KC];
+    __shared__ f32x4 box_s[4][KC];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + w + 1;  // class 0 is background
+    const int b = blockIdx.y;
+    if (c >= NC) return;                   // whole wave leaves; nothing below waits on other waves
+    unsigned long long* keys = keys_s[w];
+    f32x4* bs = box_s[w];
+    const float* sc = scores_t + ((int64_t)b * NC + c) * A;
+    const int written = wave_select_topk<PER>(sc, A, score_thresh, topk, [&](int slot, uint32_t k, int i) {
+        if (slot < KC) keys[slot] = make_key(k, (uint32_t)i);
+    });
     const int m = written < KC ? written : KC;
     int p2 = 64;
     while (p2 < m) p2 <<= 1;
@@ -633,6 +704,203 @@ __global__ void __launch_bounds__(256) ssd_class_nms_wave_kernel(const float* __
     if (lane == 0) out.count[seg] = nkept < out.kmax ? nkept : out.kmax;
 }
 
+// ================================================================ SSD postprocess, image-greedy form
+// The reference's tail (per class: score > t, topk; concatenate; batched_nms; [:N]) only ever
+// reports the first N kept candidates in (score desc, concatenation position asc) order.  Greedy
+// NMS of one class depends only on that class's higher-ranked candidates, so walking the
+// concatenated candidates in that global order, class by class greedy, and stopping once N are
+// kept yields exactly the reference's output while touching ~N..2N candidates instead of every
+// class's full top-k (SSD: 90 x 300).
+//
+// Stage 1, ssd_class_select_kernel: one wave per (image, class) writes the class's candidate set
+// in index order into a fixed-stride pool [B][NC-1][topk] (key = score bits, 0 = empty; ref =
+// anchor).  Pool position (class, slot) is the concatenation order among equal scores.
+template <int PER>
+__global__ void __launch_bounds__(256) ssd_class_select_kernel(const float* __restrict__ scores_t, int A, int NC,
+                                                               float score_thresh, int topk,
+                                                               uint32_t* __restrict__ pool_key,
+                                                               int* __restrict__ pool_ref) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + w + 1;
+    const int b = blockIdx.y;
+    if (c >= NC) return;
+    const int64_t base = ((int64_t)b * (NC - 1) + (c - 1)) * topk;
+    uint32_t* pk = pool_key + base;
+    int* pr = pool_ref + base;
+    const int written = wave_select_topk<PER>(scores_t + ((int64_t)b * NC + c) * A, A, score_thresh, topk,
+                                              [&](int slot, uint32_t k, int i) {
+                                                  if (slot < topk) {
+                                                      pk[slot] = k;
+                                                      pr[slot] = i;
+                                                  }
+                                              });
+    for (int t = (written < topk ? written : topk) + lane; t < topk; t += 64) pk[t] = 0u;
+}
+
+// Stage 2, ssd_image_nms_kernel: one workgroup per image.  The pool's keys live in VGPRs (element
+// i = threadIdx.x + NT*j); each round takes the exact next M candidates in global order
+// (register bisection + ordered compaction, ties lowest pool position first), sorts them, and
+// runs greedy NMS per class: wave w owns classes w, w+NW, ...; for each 64-candidate chunk of
+// sorted order it first drops candidates overlapping the class's already-kept boxes (kept lists
+// live in LDS as linked segments), then resolves the chunk lazily (earliest alive is kept and
+// suppresses the alive ones it overlaps).  Kept candidates are emitted in sorted order until N.
+template <int M, int KCAP, int PW>
+struct ImgSmem {
+    unsigned long long keys[M];
+    f32x4 box[M];
+    int cls[M];
+    int kflag[M];
+    f32x4 kbox[KCAP];
+    int seg_base[KCAP], seg_n[KCAP], seg_next[KCAP];
+    int head[SSD_MAXNC];
+    int hist[SSD_MAXNC];
+    uint32_t done[PW];
+    int wsum[32];
+    int red[32];
+    int misc[8];
+};
+
+template <int NT, int PER, int M, int KCAP>
+__global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __restrict__ pool_key,
+                                                           const int* __restrict__ pool_ref,
+                                                           const f32x4* __restrict__ boxes, int A, int NS, int topk,
+                                                           int N, IouThr iou, const float* __restrict__ ratio,
+                                                           float* __restrict__ out_box, float* __restrict__ out_score,
+                                                           int64_t* __restrict__ out_label, int* __restrict__ out_count) {
+    static_assert(M == NT, "one sorted candidate per thread");
+    constexpr int PW = NT * PER / 32;
+    constexpr int NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    ImgSmem<M, KCAP, PW>& S = *reinterpret_cast<ImgSmem<M, KCAP, PW>*>(smem_raw);
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const int n = NS * topk;
+    const uint32_t* pk = pool_key + (int64_t)b * n;
+    const int* pr = pool_ref + (int64_t)b * n;
+    const f32x4* bx = boxes + (int64_t)b * A;
+
+    uint32_t kr[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int i = tid + NT * j;
+        const uint32_t k = pk[i < n ? i : n - 1];  // clamped: loads stay independent
+        kr[j] = i < n ? k : 0u;
+    }
+    for (int t = tid; t < PW; t += NT) S.done[t] = 0u;
+    for (int t = tid; t < NS; t += NT) S.head[t] = -1;
+    if (tid == 0) {
+        S.misc[0] = 0;  // kept boxes stored
+        S.misc[1] = 0;  // segments stored
+    }
+    float rw = 1.f, rh = 1.f;
+    if (ratio) {
+        rw = ratio[2 * b];
+        rh = ratio[2 * b + 1];
+    }
+    int total = 0;
+    while (true) {
+        const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red);
+        if (m == 0) break;
+        for (int t = tid; t < NS; t += NT) S.hist[t] = 0;
+        if (tid < m) {
+            const int i = key_index(S.keys[tid]);
+            atomicOr(&S.done[i >> 5], 1u << (i & 31));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = tid + NT * j;
+            if (kr[j] && ((S.done[i >> 5] >> (i & 31)) & 1u)) kr[j] = 0u;
+        }
+        bitonic_desc<NT>(S.keys, nullptr, m);
+        if (tid < m) {
+            const int i = key_index(S.keys[tid]);
+            const int c = i / topk;
+            S.box[tid] = bx[pr[i]];
+            S.cls[tid] = c;
+            S.kflag[tid] = 0;
+            atomicAdd(&S.hist[c], 1);
+        }
+        __syncthreads();
+        for (int c = wv; c < NS; c += NW) {
+            int remaining = S.hist[c];
+            for (int base = 0; base < m && remaining > 0; base += 64) {
+                const int t = base + lane;
+                const bool in = t < m && S.cls[t] == c;
+                const unsigned long long inm = __ballot(in);
+                if (!inm) continue;
+                remaining -= __popcll(inm);
+                const f32x4 q = in ? S.box[t] : f32x4{0.f, 0.f, 0.f, 0.f};
+                const float aq = (q.z - q.x) * (q.w - q.y);
+                bool alive = in;
+                for (int sg = S.head[c]; sg >= 0 && __ballot(alive); sg = S.seg_next[sg]) {
+                    const int sb = S.seg_base[sg], sn = S.seg_n[sg];
+                    for (int e = 0; e < sn; ++e) {
+                        const f32x4 kb = S.kbox[sb + e];
+                        const float ka = (kb.z - kb.x) * (kb.w - kb.y);
+                        if (alive && iou_gt(kb, ka, q, aq, iou)) alive = false;
+                    }
+                }
+                unsigned long long keptm = 0ull;
+                while (true) {
+                    const unsigned long long am = __ballot(alive);
+                    if (!am) break;
+                    const int l = __builtin_ctzll(am);
+                    keptm |= 1ull << l;
+                    f32x4 kb;
+                    kb.x = __shfl(q.x, l);
+                    kb.y = __shfl(q.y, l);
+                    kb.z = __shfl(q.z, l);
+                    kb.w = __shfl(q.w, l);
+                    const float ka = __shfl(aq, l);
+                    if (lane == l) alive = false;
+                    else if (alive && iou_gt(kb, ka, q, aq, iou)) alive = false;
+                }
+                if (keptm) {
+                    const int nk = __popcll(keptm);
+                    int sb = 0, sg = 0;
+                    if (lane == 0) {
+                        sb = atomicAdd(&S.misc[0], nk);
+                        sg = atomicAdd(&S.misc[1], 1);
+                    }
+                    sb = __shfl(sb, 0);
+                    sg = __shfl(sg, 0);
+                    if ((keptm >> lane) & 1ull) {
+                        S.kbox[sb + __popcll(keptm & lt_mask)] = q;
+                        S.kflag[t] = 1;
+                    }
+                    if (lane == 0) {
+                        S.seg_base[sg] = sb;
+                        S.seg_n[sg] = nk;
+                        S.seg_next[sg] = S.head[c];
+                        S.head[c] = sg;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+        __syncthreads();
+        const bool kf = tid < m && S.kflag[tid];
+        int tot;
+        const int pos = BlockScan<NT>::exclusive(kf ? 1 : 0, S.wsum, tot);
+        if (kf && total + pos < N) {
+            const f32x4 q = S.box[tid];
+            const int64_t o = (int64_t)b * N + total + pos;
+            float* ob = out_box + o * 4;
+            ob[0] = q.x * rw;
+            ob[1] = q.y * rh;
+            ob[2] = q.z * rw;
+            ob[3] = q.w * rh;
+            out_score[o] = __uint_as_float((uint32_t)(S.keys[tid] >> 32));
+            if (out_label) out_label[o] = (int64_t)(S.cls[tid] + 1);
+        }
+        total += tot;
+        if (total >= N || m < M) break;
+    }
+    if (tid == 0) out_count[b] = total < N ? total : N;
+}
+
 // ================================================================ RPN per-level selection
 
 template <int NT, int KC>
@@ -687,10 +955,9 @@ __global__ void __launch_bounds__(NT) box_class_nms_kernel(const float* __restri
     const f32x4* bx = boxes + (int64_t)b * R * NC + c;
     auto fkey = [&](int i, uint32_t& k) -> bool {
         const float s = sc[(int64_t)i * NC];
+        const f32x4 q = bx[(int64_t)i * NC];  // loaded unconditionally (no dependent round trip)
         k = __float_as_uint(s);
-        if (!(s > score_thresh)) return false;
-        const f32x4 q = bx[(int64_t)i * NC];
-        return (q.z - q.x) >= min_size && (q.w - q.y) >= min_size;
+        return (s > score_thresh) & ((q.z - q.x) >= min_size) & ((q.w - q.y) >= min_size);
     };
     const int m = compact<NT>(n, 0u, true, 0, KC, fkey, S.keys, S.wsum);
     bitonic_desc<NT>(S.keys, nullptr, m);
@@ -776,11 +1043,22 @@ __global__ void __launch_bounds__(NT) merge_topk_kernel(MergeParams P) {
     };
     int m0;
     if (n <= NT * PER) {
-        uint32_t kr[PER];
+        // all record offsets first (LDS searches), then the global loads back to back
+        int fo[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int i = threadIdx.x + NT * j;
-            kr[j] = i < n ? float_key(P.score[base_off + flat(i)]) : 0u;
+            fo[j] = flat(i < n ? i : (n > 0 ? n - 1 : 0));
+        }
+        float v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) v[j] = P.score[base_off + fo[j]];
+        uint32_t kr[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            asm volatile("" : "+v"(v[j]));  // keeps every load unconditional (not sunk into a branch)
+            const int i = threadIdx.x + NT * j;
+            kr[j] = i < n ? float_key(v[j]) : 0u;
         }
         // every key > T plus all ties (up to capacity); ties are then ordered by tiebreak
         m0 = select_topk_regs<NT, PER>(kr, P.N, KC, S.keys, S.wsum, S.misc, true);
@@ -889,6 +1167,27 @@ int ssd_class_nms_launch(const float* scores_t, const float* boxes, int B, int A
     EDGEDET_REQUIRE(A <= 64 * PER, "ssd_class_nms: at most 3328 anchors per image");
     hipLaunchKernelGGL((ssd_class_nms_wave_kernel<PER, KC>), dim3((unsigned)cdiv(NC - 1, 4), B), dim3(256), 0, s,
                        scores_t, (const f32x4*)boxes, A, NC, score_thresh, topk, make_iou_thr(iou), out);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+int ssd_postprocess_launch(const SsdPostParams& P, hipStream_t s) {
+    EDGEDET_REQUIRE(P.scores_t && P.boxes && P.pool_key && P.pool_ref && P.out_box && P.out_score && P.out_count,
+                    "ssd_postprocess: null pointer");
+    constexpr int PER_A = 52, NT = 512, PER = 54, M = 512, KCAP = 1536;
+    EDGEDET_REQUIRE(P.A > 0 && P.A <= 64 * PER_A, "ssd_postprocess: at most 3328 anchors per image");
+    EDGEDET_REQUIRE(P.NC >= 2 && P.NC <= SSD_MAXNC, "ssd_postprocess: 2..128 classes");
+    EDGEDET_REQUIRE(P.topk > 0 && (int64_t)(P.NC - 1) * P.topk <= (int64_t)NT * PER,
+                    "ssd_postprocess: (classes-1) * topk must be <= 27648");
+    EDGEDET_REQUIRE(P.N > 0 && P.N + M <= KCAP, "ssd_postprocess: detections per image must be <= 1024");
+    hipLaunchKernelGGL(ssd_class_select_kernel<PER_A>, dim3((unsigned)cdiv(P.NC - 1, 4), P.B), dim3(256), 0, s,
+                       P.scores_t, P.A, P.NC, P.score_thresh, P.topk, P.pool_key, P.pool_ref);
+    EDGEDET_LAUNCH_CHECK();
+    auto k = ssd_image_nms_kernel<NT, PER, M, KCAP>;
+    const size_t lds = sizeof(ImgSmem<M, KCAP, NT * PER / 32>);
+    if (set_lds(k, lds)) return -2;
+    hipLaunchKernelGGL(k, dim3(P.B), dim3(NT), lds, s, P.pool_key, P.pool_ref, (const f32x4*)P.boxes, P.A, P.NC - 1,
+                       P.topk, P.N, make_iou_thr(P.iou), P.ratio, P.out_box, P.out_score, P.out_label, P.out_count);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

@@ -12,9 +12,11 @@
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
-//   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act
-//   CHANNEL_MEAN   p0 x[B,HW,C]; p1 part[B,16,C] (partial sums over 16 pixel splits); i0..2 B,HW,C
-//   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; i0..3 B,C,S,HW
+//   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
+//                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act
+//   CHANNEL_MEAN   p0 x[B,HW,C]; p1 mean[B,C]; i0..2 B,HW,C
+//   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; p6 hidden[B,S];
+//                  i0..3 B,C,S,HW
 //   MAXPOOL        p0 x; p1 y; i0..8 B,H,W,C,Ho,Wo,K,stride,pad
 //   SSD_SCORES     p0 logits[B,A,NC]; p1 reg[B,A,4]; p2 anchors[A,4]; p3 scores_t[B,NC,A];
 //                  p4 boxes[B,A,4]; i0..2 B,A,NC; f0,f1 img_h,img_w
@@ -31,6 +33,8 @@
 //                  f0,f1 img_h,img_w
 //   BOX_CLASS_NMS  p0 scores; p1 boxes; p2 counts; p3..7 records; i0..3 B,R,NC,kmax;
 //                  f0 score_thresh; f1 min_size; d0 iou
+//   SSD_POSTPROCESS p0 scores_t; p1 boxes; p2 pool_key; p3 pool_ref; p4 ratio|0; p5 out_box; p6 out_score;
+//                  p7 out_label|0; p8 out_count; i0..4 B,A,NC,topk,N; f0 score_thresh; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 #include <mutex>
 #include <string>
@@ -123,6 +127,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.w = P<const float>(o, 1);
             p.bias = P<const float>(o, 2);
             p.y = P<float>(o, 3);
+            p.part = P<float>(o, 4);
             p.B = (int)I[0];
             p.H = (int)I[1];
             p.W = (int)I[2];
@@ -139,7 +144,8 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             return channel_mean_launch(P<const float>(o, 0), P<float>(o, 1), (int)I[0], (int)I[1], (int)I[2], s);
         case EDGEDET_OP_SE_FC:
             return se_fc_launch(P<const float>(o, 0), P<const float>(o, 1), P<const float>(o, 2), P<const float>(o, 3),
-                                P<const float>(o, 4), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2], (int)I[3], s);
+                                P<const float>(o, 4), P<float>(o, 6), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2],
+                                (int)I[3], s);
         case EDGEDET_OP_MAXPOOL: {
             PoolParams p{};
             p.x = P<const float>(o, 0);
@@ -230,6 +236,26 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
         case EDGEDET_OP_BOX_CLASS_NMS:
             return box_class_nms_launch(P<const float>(o, 0), P<const float>(o, 1), P<const int>(o, 2), (int)I[0],
                                         (int)I[1], (int)I[2], o.f[0], o.f[1], o.d[0], seg_out(o, 3, (int)I[3]), s);
+        case EDGEDET_OP_SSD_POSTPROCESS: {
+            SsdPostParams p{};
+            p.scores_t = P<const float>(o, 0);
+            p.boxes = P<const float>(o, 1);
+            p.pool_key = P<uint32_t>(o, 2);
+            p.pool_ref = P<int>(o, 3);
+            p.ratio = P<const float>(o, 4);
+            p.out_box = P<float>(o, 5);
+            p.out_score = P<float>(o, 6);
+            p.out_label = P<int64_t>(o, 7);
+            p.out_count = P<int>(o, 8);
+            p.B = (int)I[0];
+            p.A = (int)I[1];
+            p.NC = (int)I[2];
+            p.topk = (int)I[3];
+            p.N = (int)I[4];
+            p.score_thresh = o.f[0];
+            p.iou = o.d[0];
+            return ssd_postprocess_launch(p, s);
+        }
         default:
             set_error("edgedet: unknown op kind " + std::to_string(o.kind));
             return -1;

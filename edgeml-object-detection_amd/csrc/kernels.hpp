@@ -4,6 +4,8 @@
 
 namespace edgedet {
 
+constexpr int SE_PARTS = 16;  // pixel splits of the SE squeeze partial sums
+
 struct ConvParams {
     const float* x;
     const float* w;
@@ -34,6 +36,7 @@ struct DwParams {
     const float* w;  // [K*K][C]
     const float* bias;
     float* y;        // [B][Ho][Wo][C]
+    float* part;     // optional SE squeeze partial sums [B][SE_PARTS][C]
     int B, H, W, C, Ho, Wo, K, stride, pad, act;
 };
 
@@ -101,13 +104,27 @@ struct MergeParams {
     int* out_count;      // [B]
 };
 
+struct SsdPostParams {
+    const float* scores_t;  // [B][NC][A] class probabilities
+    const float* boxes;     // [B][A][4] decoded, clipped
+    uint32_t* pool_key;     // [B][NC-1][topk] scratch
+    int* pool_ref;          // [B][NC-1][topk] scratch
+    const float* ratio;     // [B][2] or null
+    float* out_box;         // [B][N][4]
+    float* out_score;       // [B][N]
+    int64_t* out_label;     // [B][N] or null
+    int* out_count;         // [B]
+    int B, A, NC, topk, N;
+    float score_thresh;
+    double iou;
+};
+
 int conv_launch(ConvParams p, int tile, hipStream_t s);
 int preprocess_launch(const PreParams& p, hipStream_t s);
 int dwconv_launch(const DwParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);
-int se_fc_launch(const float* mean, const float* w1, const float* b1, const float* w2t, const float* b2,
-                 float* scale, int B, int C, int S, int HW, hipStream_t s);
-constexpr int SE_PARTS = 16;  // pixel splits of the SE squeeze (layers.hip SE_SPLITS)
+int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
+                 float* hidden, float* scale, int B, int C, int S, int HW, hipStream_t s);
 int maxpool_launch(const PoolParams& p, hipStream_t s);
 int roi_align_launch(const RoiParams& p, hipStream_t s);
 int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,
@@ -120,5 +137,6 @@ int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s);
 int box_class_nms_launch(const float* scores, const float* boxes, const int* counts, int B, int R, int NC,
                          float score_thresh, float min_size, double iou, SegOut out, hipStream_t s);
 int merge_topk_launch(const MergeParams& P, int B, hipStream_t s);
+int ssd_postprocess_launch(const SsdPostParams& P, hipStream_t s);
 
 }  // namespace edgedet

@@ -4,7 +4,7 @@
 //                (align_corners=False), zero pad to the batch size        SURVEY.md App. A.0, row a6
 //   dwconv       depthwise conv + folded BN + act (MobileNetV3 / SSDLite)  App. A.1, rows a7/a8
 //   channel_mean adaptive_avg_pool2d(1) of SqueezeExcitation               App. A.1 step 2
-//   se_fc        SE fc1 -> ReLU -> fc2 -> Hardsigmoid (per image)          App. A.1 step 2
+//   se_fc        SE fc1 -> ReLU -> fc2 -> Hardsigmoid (batched GEMVs)       App. A.1 step 2
 //   maxpool      ResNet stem max_pool2d(3,2,1); FPN LastLevelMaxPool(1,2,0) App. A.2 steps 2-3
 //   roi_align    MultiScaleRoIAlign: LevelMapper + roi_align(7x7, sr=2, aligned=False)
 //                                                                          App. A.2 step 5, row a13
@@ -99,9 +99,197 @@ __global__ void dwconv_kernel(DwParams p) {
     *reinterpret_cast<f32x4*>(p.y + pix * p.C + c) = o;
 }
 
+// Depthwise conv + folded BN + act that also emits the SqueezeExcitation squeeze: partial channel
+// sums part[b][s][c] over pixel split s (SE_PARTS splits, reduced in fixed order by se_fc1_kernel).
+// grid (cdiv(C, 64), SE_PARTS, B); block 256 = 16 channel quads x 16 pixel lanes, so one wave
+// writes 4 pixels x 256 contiguous bytes.
+__global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
+    __shared__ f32x4 red[16][16];
+    const int cq = threadIdx.x & 15, pl = threadIdx.x >> 4;
+    const int c = blockIdx.x * 64 + cq * 4;
+    const int sidx = blockIdx.y, b = blockIdx.z;
+    const int HWo = p.Ho * p.Wo;
+    const int p0 = (int)((int64_t)sidx * HWo / SE_PARTS), p1 = (int)((int64_t)(sidx + 1) * HWo / SE_PARTS);
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    if (c < p.C) {
+        const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+        for (int pix = p0 + pl; pix < p1; pix += 16) {
+            const int oh = pix / p.Wo, ow = pix - oh * p.Wo;
+            const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int kh = 0; kh < p.K; ++kh) {
+                const int ih = ih0 + kh;
+                if ((unsigned)ih >= (unsigned)p.H) continue;
+                for (int kw = 0; kw < p.K; ++kw) {
+                    const int iw = iw0 + kw;
+                    if ((unsigned)iw >= (unsigned)p.W) continue;
+                    const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * p.C);
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * p.K + kw) * p.C + c);
+                    acc.x = fmaf(xv.x, wv.x, acc.x);
+                    acc.y = fmaf(xv.y, wv.y, acc.y);
+                    acc.z = fmaf(xv.z, wv.z, acc.z);
+                    acc.w = fmaf(xv.w, wv.w, acc.w);
+                }
+            }
+            f32x4 o;
+            o.x = apply_act(acc.x + bv.x, p.act);
+            o.y = apply_act(acc.y + bv.y, p.act);
+            o.z = apply_act(acc.z + bv.z, p.act);
+            o.w = apply_act(acc.w + bv.w, p.act);
+            *reinterpret_cast<f32x4*>(p.y + ((int64_t)b * HWo + pix) * p.C + c) = o;
+            sum += o;
+        }
+    }
+    red[pl][cq] = sum;
+    __syncthreads();
+    if (pl == 0 && c < p.C) {
+        f32x4 t = red[0][cq];
+        for (int q = 1; q < 16; ++q) t += red[q][cq];
+        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * SE_PARTS + sidx) * p.C + c) = t;
+    }
+}
+
+// Register-blocked depthwise conv for the MobileNetV3 shapes (K in {3,5}, stride in {1,2}): a
+// thread computes PW horizontally adjacent outputs of one channel quad, loading each input row
+// segment once into registers ((PW-1)*S+K f32x4 per kernel row instead of PW*K), so L1/TA traffic
+// per output drops by ~K/(1+(K-1)/PW).  Accumulation order per output is (kh, kw) as in the
+// scalar kernel.  SE variant: grid (cdiv(C/4,16), SE_PARTS, B), block = 16 quads x 16 group lanes,
+// partial sums per pixel-group split (see dwconv_se_kernel).
+template <int K, int S, int PW>
+__device__ __forceinline__ void dw_group(const DwParams& p, const float* __restrict__ xb, int oh, int ow0, int c,
+                                         f32x4 (&acc)[PW]) {
+    constexpr int IW = (PW - 1) * S + K;
+#pragma unroll
+    for (int o = 0; o < PW; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ih0 = oh * S - p.pad, iw0 = ow0 * S - p.pad;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+        const int ih = ih0 + kh;
+        if ((unsigned)ih >= (unsigned)p.H) continue;
+        const float* row = xb + (int64_t)ih * p.W * p.C;
+        f32x4 xin[IW];
+#pragma unroll
+        for (int j = 0; j < IW; ++j) {
+            const int iw = iw0 + j;
+            xin[j] = (unsigned)iw < (unsigned)p.W ? *reinterpret_cast<const f32x4*>(row + (int64_t)iw * p.C)
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+            const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * K + kw) * p.C + c);
+#pragma unroll
+            for (int o = 0; o < PW; ++o) {
+                const f32x4 xv = xin[o * S + kw];
+                acc[o].x = fmaf(xv.x, wv.x, acc[o].x);
+                acc[o].y = fmaf(xv.y, wv.y, acc[o].y);
+                acc[o].z = fmaf(xv.z, wv.z, acc[o].z);
+                acc[o].w = fmaf(xv.w, wv.w, acc[o].w);
+            }
+        }
+    }
+}
+
+template <int K, int S, int PW>
+__global__ void __launch_bounds__(256) dwconv_rb_kernel(DwParams p, int nq, int nwg) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
+    if (idx >= total) return;
+    const int q = (int)(idx % nq);
+    int64_t r = idx / nq;
+    const int wg = (int)(r % nwg);
+    r /= nwg;
+    const int oh = (int)(r % p.Ho);
+    const int b = (int)(r / p.Ho);
+    const int c = q * 4, ow0 = wg * PW;
+    f32x4 acc[PW];
+    dw_group<K, S, PW>(p, p.x + (int64_t)b * p.H * p.W * p.C + c, oh, ow0, c, acc);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+    float* yb = p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow0) * p.C + c;
+    const int act = p.act;
+#pragma unroll
+    for (int o = 0; o < PW; ++o) {
+        if (ow0 + o < p.Wo) {
+            f32x4 v;
+            v.x = apply_act(acc[o].x + bv.x, act);
+            v.y = apply_act(acc[o].y + bv.y, act);
+            v.z = apply_act(acc[o].z + bv.z, act);
+            v.w = apply_act(acc[o].w + bv.w, act);
+            *reinterpret_cast<f32x4*>(yb + (int64_t)o * p.C) = v;
+        }
+    }
+}
+
+template <int K, int S, int PW>
+__global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, int nwg) {
+    __shared__ f32x4 red[16][16];
+    const int ql = threadIdx.x & 15, gl = threadIdx.x >> 4;
+    const int q = blockIdx.x * 16 + ql;
+    const int c = q * 4;
+    const int sidx = blockIdx.y, b = blockIdx.z;
+    const int G = p.Ho * nwg;
+    const int g0 = (int)((int64_t)sidx * G / SE_PARTS), g1 = (int)((int64_t)(sidx + 1) * G / SE_PARTS);
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    if (q < nq) {
+        const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+        const int act = p.act;
+        for (int g = g0 + gl; g < g1; g += 16) {
+            const int oh = g / nwg, ow0 = (g - oh * nwg) * PW;
+            f32x4 acc[PW];
+            dw_group<K, S, PW>(p, xb, oh, ow0, c, acc);
+            float* yb = p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow0) * p.C + c;
+#pragma unroll
+            for (int o = 0; o < PW; ++o) {
+                if (ow0 + o < p.Wo) {
+                    f32x4 v;
+                    v.x = apply_act(acc[o].x + bv.x, act);
+                    v.y = apply_act(acc[o].y + bv.y, act);
+                    v.z = apply_act(acc[o].z + bv.z, act);
+                    v.w = apply_act(acc[o].w + bv.w, act);
+                    *reinterpret_cast<f32x4*>(yb + (int64_t)o * p.C) = v;
+                    sum += v;
+                }
+            }
+        }
+    }
+    red[gl][ql] = sum;
+    __syncthreads();
+    if (gl == 0 && q < nq) {
+        f32x4 t = red[0][ql];
+        for (int k = 1; k < 16; ++k) t += red[k][ql];
+        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * SE_PARTS + sidx) * p.C + c) = t;
+    }
+}
+
+template <int K, int S>
+static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
+    constexpr int PW = 4;
+    const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
+    if (p.part) {
+        hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW>), dim3((unsigned)cdiv(nq, 16), SE_PARTS, p.B), dim3(256), 0,
+                           s, p, nq, nwg);
+    } else {
+        const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
+        hipLaunchKernelGGL((dwconv_rb_kernel<K, S, PW>), dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, nq,
+                           nwg);
+    }
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
 int dwconv_launch(const DwParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
+    if (p.K == 3 && p.stride == 1) return dwconv_rb_launch<3, 1>(p, s);
+    if (p.K == 3 && p.stride == 2) return dwconv_rb_launch<3, 2>(p, s);
+    if (p.K == 5 && p.stride == 1) return dwconv_rb_launch<5, 1>(p, s);
+    if (p.K == 5 && p.stride == 2) return dwconv_rb_launch<5, 2>(p, s);
+    if (p.part) {
+        hipLaunchKernelGGL(dwconv_se_kernel, dim3((unsigned)cdiv(p.C, 64), SE_PARTS, p.B), dim3(256), 0, s, p);
+        EDGEDET_LAUNCH_CHECK();
+        return 0;
+    }
     const int64_t total = (int64_t)p.B * p.Ho * p.Wo * (p.C / 4);
     hipLaunchKernelGGL(dwconv_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
@@ -109,91 +297,126 @@ int dwconv_launch(const DwParams& p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------ SE squeeze
-// Partial channel sums: grid (cdiv(C, 64), B, S) with block 256 = 64 channels x 4 pixel groups; split s
-// covers pixels [s*HW/S, (s+1)*HW/S).  part[b][s][c] is reduced in fixed order by se_fc_kernel
-// (deterministic, no atomics).
-
-__global__ void channel_sum_kernel(const float* __restrict__ x, float* __restrict__ part, int HW, int C, int S) {
+// Standalone adaptive_avg_pool2d(1) for an SE whose producer is not a depthwise conv: grid
+// (cdiv(C, 64), B), block 256 = 64 channels x 4 pixel groups, fixed-order reduction.  (The SSDLite
+// blocks use the squeeze fused into dwconv_se_kernel instead.)
+__global__ void channel_mean_kernel(const float* __restrict__ x, float* __restrict__ mean, int HW, int C) {
     __shared__ float red[4][64];
-    const int b = blockIdx.y, sidx = blockIdx.z;
+    const int b = blockIdx.y;
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
-    const int p0 = (int)((int64_t)sidx * HW / S), p1 = (int)((int64_t)(sidx + 1) * HW / S);
     float acc = 0.f;
     if (c < C) {
         const float* xb = x + (int64_t)b * HW * C + c;
-        for (int i = p0 + g; i < p1; i += 4) acc += xb[(int64_t)i * C];
+        for (int i = g; i < HW; i += 4) acc += xb[(int64_t)i * C];
     }
     red[g][cl] = acc;
     __syncthreads();
     if (g == 0 && c < C)
-        part[((int64_t)b * S + sidx) * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+        mean[(int64_t)b * C + c] = (((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]) / (float)HW;
 }
 
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s) {
     EDGEDET_REQUIRE(x && out, "channel_mean: null pointer");
-    hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)cdiv(C, 64), B, SE_PARTS), dim3(256), 0, s, x, out, HW, C,
-                       SE_PARTS);
+    hipLaunchKernelGGL(channel_mean_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), 0, s, x, out, HW, C);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
 
 // ------------------------------------------------------------------------------ SE excitation
-// grid (cdiv(C, 64), B): every block recomputes the (small) fc1 of its image from the partial sums
-// part [B][SE_PARTS][C] (mean = sum / HW, fixed reduction order), then evaluates fc2 + Hardsigmoid
-// for its 64 channels.  w1 [S][C] (fc1 as stored), w2t [S][C] (fc2 transposed).  fc1 splits the C
-// reduction over the 64 lanes of a wave; fc2 splits the S reduction over 4 waves.
-__global__ void __launch_bounds__(256) se_fc_kernel(const float* __restrict__ part, const float* __restrict__ w1,
-                                                    const float* __restrict__ b1, const float* __restrict__ w2t,
-                                                    const float* __restrict__ b2, float* __restrict__ scale, int C,
-                                                    int S, int HW) {
-    extern __shared__ float sm[];
-    float* m = sm;             // [C]
-    float* s1 = sm + C;        // [S]
-    float* red = s1 + S;       // [256]
-    const int b = blockIdx.y;
-    const int tid = threadIdx.x;
-    for (int c = tid; c < C; c += 256) {
-        float acc = 0.f;
-        for (int k = 0; k < SE_PARTS; ++k) acc += part[((int64_t)b * SE_PARTS + k) * C + c];
-        m[c] = acc / (float)HW;
-    }
-    __syncthreads();
-    // fc1: wave w owns outputs j = w, w+4, ...; its 64 lanes split the C reduction (fixed order:
-    // lane-strided partial sums, then a butterfly)
-    const int lane = tid & 63, wv = tid >> 6;
-    for (int j = wv; j < S; j += 4) {
-        float a = 0.f;
-        for (int c = lane; c < C; c += 64) a = fmaf(w1[(int64_t)j * C + c], m[c], a);
+// All B images share the SE weights, so the excitation runs as two small batched GEMVs tiled over
+// many workgroups; each workgroup stages its operands in LDS with independent loads (one or two
+// memory round trips instead of a dependent chain per element):
+//   se_fc1: tile 8 images x 8 squeeze outputs.  mean[b][c] = (sum of the SE_PARTS partial sums in
+//           fixed order) / HW for its 8 images, w1 rows [8][C]; hidden = relu(b1 + w1 . mean),
+//           each output reduced over C quarters by 4 threads (fixed order).
+//   se_fc2: tile 8 images x 64 channels.  hidden[8][S] and w2t [128-row chunks][64] in LDS;
+//           scale = hardsigmoid(b2 + w2 . hidden), 2 outputs per thread.
+constexpr int SE1_BB = 8, SE1_SB = 8, SE2_BB = 8, SE2_SCH = 128;
+constexpr int SE_CMAX = 1024, SE_SMAX = 512;
+
+__global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ part, const float* __restrict__ w1,
+                                                     const float* __restrict__ b1, float* __restrict__ hidden, int B,
+                                                     int C, int S, int HW) {
+    __shared__ float ms[SE1_BB * SE_CMAX];
+    __shared__ float ws[SE1_SB * SE_CMAX];
+    const int s0 = blockIdx.x * SE1_SB, b0 = blockIdx.y * SE1_BB;
+    const int nb = min(SE1_BB, B - b0), ns = min(SE1_SB, S - s0);
+    const float inv = 1.f / (float)HW;
+    for (int t = threadIdx.x; t < nb * C; t += 256) {
+        const int bl = t / C, c = t - bl * C;
+        const float* pp = part + ((int64_t)(b0 + bl) * SE_PARTS) * C + c;
+        float v[SE_PARTS];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-        if (lane == 0) {
-            a += b1[j];
-            s1[j] = a > 0.f ? a : 0.f;
-        }
+        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)k * C];
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < SE_PARTS; ++k) acc += v[k];
+        ms[t] = acc * inv;
     }
+    for (int t = threadIdx.x; t < ns * C; t += 256) ws[t] = w1[(int64_t)s0 * C + t];
     __syncthreads();
-    const int cl = tid & 63, g = tid >> 6;
-    const int c = blockIdx.x * 64 + cl;
-    float a = 0.f;
-    if (c < C)
-        for (int j = g; j < S; j += 4) a = fmaf(w2t[(int64_t)j * C + c], s1[j], a);
-    red[tid] = a;
-    __syncthreads();
-    if (g == 0 && c < C) {
-        const float v = ((red[cl] + red[64 + cl]) + red[128 + cl]) + red[192 + cl];
-        scale[(int64_t)b * C + c] = apply_act(v + b2[c], ACT_HSIGMOID);
+    // 64 outputs (bl = o & 7, sl = o >> 3), 4 threads each over C quarters
+    const int o = threadIdx.x >> 2, h = threadIdx.x & 3;
+    const int bl = o & 7, sl = o >> 3;
+    const int ch = (C + 3) >> 2;
+    const int c0 = h * ch, c1 = min(C, c0 + ch);
+    float acc = 0.f;
+    if (bl < nb && sl < ns) {
+        const float* mr = ms + bl * C;
+        const float* wr = ws + sl * C;
+        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (h == 0 && bl < nb && sl < ns) {
+        const float t = acc + b1[s0 + sl];
+        hidden[(int64_t)(b0 + bl) * S + s0 + sl] = t > 0.f ? t : 0.f;
     }
 }
 
-int se_fc_launch(const float* mean, const float* w1, const float* b1, const float* w2t, const float* b2,
-                 float* scale, int B, int C, int S, int HW, hipStream_t s) {
-    EDGEDET_REQUIRE(mean && w1 && b1 && w2t && b2 && scale, "se_fc: null pointer");
-    EDGEDET_REQUIRE(S >= 1 && S <= 256, "se_fc: squeeze width must be in [1, 256]");
-    const size_t lds = (size_t)(C + S + 256) * sizeof(float);
-    EDGEDET_REQUIRE(lds <= 60 * 1024, "se_fc: too many channels");
-    hipLaunchKernelGGL(se_fc_kernel, dim3((unsigned)cdiv(C, 64), B), dim3(256), lds, s, mean, w1, b1, w2t, b2, scale,
-                       C, S, HW);
+__global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ hidden, const float* __restrict__ w2t,
+                                                     const float* __restrict__ b2, float* __restrict__ scale, int B,
+                                                     int C, int S) {
+    __shared__ float hs[SE2_BB * SE_SMAX];
+    __shared__ float ws[SE2_SCH * 64];
+    const int c0 = blockIdx.x * 64, b0 = blockIdx.y * SE2_BB;
+    const int nb = min(SE2_BB, B - b0), nc = min(64, C - c0);
+    for (int t = threadIdx.x; t < nb * S; t += 256) hs[t] = hidden[(int64_t)b0 * S + t];
+    const int cl = threadIdx.x & 63, bp = threadIdx.x >> 6;  // images bp and bp + 4
+    float a0 = 0.f, a1 = 0.f;
+    const float* h0 = hs + bp * S;
+    const float* h1 = hs + (bp + 4) * S;
+    for (int j0 = 0; j0 < S; j0 += SE2_SCH) {
+        const int nj = min(SE2_SCH, S - j0);
+        for (int t = threadIdx.x; t < nj * 64; t += 256) {
+            const int j = t >> 6, c = t & 63;
+            ws[t] = c < nc ? w2t[(int64_t)(j0 + j) * C + c0 + c] : 0.f;
+        }
+        __syncthreads();
+        for (int j = 0; j < nj; ++j) {
+            const float wv = ws[j * 64 + cl];
+            a0 = fmaf(wv, h0[j0 + j], a0);
+            a1 = fmaf(wv, h1[j0 + j], a1);
+        }
+        __syncthreads();
+    }
+    if (cl < nc) {
+        const float bias = b2[c0 + cl];
+        if (bp < nb) scale[(int64_t)(b0 + bp) * C + c0 + cl] = apply_act(a0 + bias, ACT_HSIGMOID);
+        if (bp + 4 < nb) scale[(int64_t)(b0 + bp + 4) * C + c0 + cl] = apply_act(a1 + bias, ACT_HSIGMOID);
+    }
+}
+
+int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
+                 float* hidden, float* scale, int B, int C, int S, int HW, hipStream_t s) {
+    EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
+    EDGEDET_REQUIRE(S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX && HW >= 1, "se_fc: C <= 1024, S <= 512");
+    hipLaunchKernelGGL(se_fc1_kernel, dim3((unsigned)cdiv(S, SE1_SB), (unsigned)cdiv(B, SE1_BB)), dim3(256), 0, s,
+                       part, w1, b1, hidden, B, C, S, HW);
+    EDGEDET_LAUNCH_CHECK();
+    hipLaunchKernelGGL(se_fc2_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(B, SE2_BB)), dim3(256), 0, s,
+                       hidden, w2t, b2, scale, B, C, S);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

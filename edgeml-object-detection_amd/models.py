@@ -157,6 +157,10 @@ class SSDLite320(_Detector):
     SIZE = 320
     SCORE_THRESH, NMS_THRESH, DETS, TOPK = 0.001, 0.55, 300, 300
     max_batch = 64
+    # "image": SSD_POSTPROCESS (class top-k pool + one global-order greedy pass per image);
+    # "class": SSD_CLASS_NMS + MERGE_TOPK (every class's top-k fully NMS'd, then merged).
+    postprocess = "image"
+    IMAGE_POOL_MAX = 512 * 54  # (classes - 1) * TOPK that fits the image kernel's registers
 
     def __init__(self, state_dict, num_classes=91, reduced_tail=None, device=None):
         if reduced_tail is None:
@@ -205,7 +209,8 @@ class SSDLite320(_Detector):
                     in_scale=in_scale, name=prefix)
             return (y, ys)
 
-        def dw(cur, prefix, k, stride, act):
+        def dw(cur, prefix, k, stride, act, se_part=False):
+            """Depthwise conv; with se_part it also emits the SE squeeze partial sums (fused)."""
             xb, xs = cur
             w, b, _, _, c = self._conv_bn(prefix + ".0.weight", prefix + ".1", self.BN_EPS)
             pad = (k - 1) // 2
@@ -213,19 +218,20 @@ class SSDLite320(_Detector):
             Wo = (xs[2] + 2 * pad - k) // stride + 1
             ys = (B, Ho, Wo, xs[3])
             y = P.buf(ys, name=prefix)
+            part = P.buf((B, ops.SE_PARTS, xs[3]), name=prefix + ".se_partial_sums") if se_part else None
             P.add(Op(ops.DWCONV, {0: B, 1: xs[1], 2: xs[2], 3: xs[3], 4: Ho, 5: Wo, 6: k, 7: stride, 8: pad,
-                                  9: ops.ACT[act]}, {0: xb, 1: w, 2: b, 3: y}, name=prefix))
-            return (y, ys)
+                                  9: ops.ACT[act]}, {0: xb, 1: w, 2: b, 3: y, 4: part}, name=prefix))
+            return (y, ys, part) if se_part else (y, ys)
 
         def se(cur, p):
-            xb, xs = cur
+            """SqueezeExcitation excitation from the partial sums the depthwise conv emitted."""
+            xb, xs, part = cur
             w1, b1, w2t, b2, sq = self._se(p)
             C = xs[3]
-            part = P.buf((B, ops.SE_PARTS, C), name=p + ".partial_sums")
             scale = P.buf((B, C), name=p + ".scale")
-            HW = xs[1] * xs[2]
-            P.add(Op(ops.CHANNEL_MEAN, {0: B, 1: HW, 2: C}, {0: xb, 1: part}, name=p + ".avgpool"))
-            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: HW}, {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale}, name=p))
+            hidden = P.buf((B, sq), name=p + ".hidden")
+            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: xs[1] * xs[2]},
+                     {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale, 6: hidden}, name=p))
             return scale
 
         def inverted_residual(cur, cnf, base):
@@ -234,10 +240,10 @@ class SSDLite320(_Detector):
             y = cur
             if pe:
                 y = conv(y, pe, 1, 1, act)
-            y = dw(y, pd, k, stride, act)
+            y = dw(y, pd, k, stride, act, se_part=use_se)
             scale = se(y, ps) if use_se else None
             res = cur[0] if (stride == 1 and cin == cout) else None
-            return conv(y, pp, 1, 1, None, res=res, in_scale=scale)
+            return conv(y[:2], pp, 1, 1, None, res=res, in_scale=scale)
 
         cfg = arch.mnv3_blocks(self.reduced_tail)
         cur = conv(cur, "backbone.features.0.0", 3, 2, "HS", cin_pad=4)
@@ -246,9 +252,9 @@ class SSDLite320(_Detector):
         _, k, exp, cout, _, act, stride = cfg[12]
         cur = conv(cur, "backbone.features.0.13", 1, 1, act)
         feats = [cur]
-        y = dw(cur, "backbone.features.1.0.1", k, stride, act)
+        y = dw(cur, "backbone.features.1.0.1", k, stride, act, se_part=True)
         scale = se(y, "backbone.features.1.0.2")
-        cur = conv(y, "backbone.features.1.0.3", 1, 1, None, in_scale=scale)
+        cur = conv(y[:2], "backbone.features.1.0.3", 1, 1, None, in_scale=scale)
         for i in (13, 14):
             cur = inverted_residual(cur, cfg[i], f"backbone.features.1.{i - 12}.block")
         cur = conv(cur, "backbone.features.1.3", 1, 1, "HS")
@@ -291,12 +297,6 @@ class SSDLite320(_Detector):
         P.add(Op(ops.SSD_SCORES, {0: B, 1: A, 2: NC}, {0: cls, 1: reg, 2: anchors, 3: scores_t, 4: boxes},
                  {0: S, 1: S}, name="postprocess.scores"))
         NS, KM = NC - 1, self.TOPK
-        rec = [P.buf((B, NS, KM, 4), name="rec.box"), P.buf((B, NS, KM), name="rec.score"),
-               P.buf((B, NS, KM), torch.int32, name="rec.tb"), P.buf((B, NS, KM), torch.int32, name="rec.label"),
-               P.buf((B, NS), torch.int32, name="rec.count")]
-        P.add(Op(ops.SSD_CLASS_NMS, {0: B, 1: A, 2: NC, 3: self.TOPK, 4: KM},
-                 {0: scores_t, 1: boxes, 2: rec[0], 3: rec[1], 4: rec[2], 5: rec[3], 6: rec[4]},
-                 {0: self.SCORE_THRESH}, {0: self.NMS_THRESH}, name="postprocess.class_nms"))
         ratio = np.tile(np.asarray([np.float32(W) / np.float32(S), np.float32(H) / np.float32(S)], np.float32),
                         (B, 1))
         ratio_b = P.const(ratio, name="ratio")
@@ -304,11 +304,27 @@ class SSDLite320(_Detector):
         P.out_score = P.buf((B, self.DETS), name="out.scores")
         P.out_label = P.buf((B, self.DETS), torch.int64, name="out.labels")
         P.out_count = P.buf((B,), torch.int32, name="out.count")
-        P.add(Op(ops.MERGE_TOPK, {0: B, 1: NS, 2: KM, 3: self.DETS},
-                 {0: rec[0], 1: rec[1], 2: rec[2], 3: rec[3], 4: rec[4], 5: ratio_b, 6: P.out_box, 7: P.out_score,
-                  8: P.out_label, 9: P.out_count}, name="postprocess.merge"))
+        if self.postprocess == "image" and NS * KM <= self.IMAGE_POOL_MAX and self.DETS <= 1024:
+            # class top-k pool + global-order greedy NMS, stopping at DETS kept (csrc/detect.hip)
+            pool_key = P.buf((B, NS, KM), torch.int32, name="pool.key")
+            pool_ref = P.buf((B, NS, KM), torch.int32, name="pool.ref")
+            P.add(Op(ops.SSD_POSTPROCESS, {0: B, 1: A, 2: NC, 3: KM, 4: self.DETS},
+                     {0: scores_t, 1: boxes, 2: pool_key, 3: pool_ref, 4: ratio_b, 5: P.out_box, 6: P.out_score,
+                      7: P.out_label, 8: P.out_count}, {0: self.SCORE_THRESH}, {0: self.NMS_THRESH},
+                     name="postprocess.nms"))
+        else:
+            rec = [P.buf((B, NS, KM, 4), name="rec.box"), P.buf((B, NS, KM), name="rec.score"),
+                   P.buf((B, NS, KM), torch.int32, name="rec.tb"), P.buf((B, NS, KM), torch.int32, name="rec.label"),
+                   P.buf((B, NS), torch.int32, name="rec.count")]
+            P.add(Op(ops.SSD_CLASS_NMS, {0: B, 1: A, 2: NC, 3: self.TOPK, 4: KM},
+                     {0: scores_t, 1: boxes, 2: rec[0], 3: rec[1], 4: rec[2], 5: rec[3], 6: rec[4]},
+                     {0: self.SCORE_THRESH}, {0: self.NMS_THRESH}, name="postprocess.class_nms"))
+            P.add(Op(ops.MERGE_TOPK, {0: B, 1: NS, 2: KM, 3: self.DETS},
+                     {0: rec[0], 1: rec[1], 2: rec[2], 3: rec[3], 4: rec[4], 5: ratio_b, 6: P.out_box,
+                      7: P.out_score, 8: P.out_label, 9: P.out_count}, name="postprocess.merge"))
         P.input = inp
         P.cls_logits, P.bbox_regression = cls, reg
+        P.scores_t, P.boxes = scores_t, boxes
         P.feats = [f[0] for f in feats]
         return P
 

@@ -19,7 +19,7 @@ OP_INTS, OP_PTRS, OP_DBLS, OP_FLTS = 48, 24, 8, 16
 # kinds (include/edgedet.h)
 MEMSET, PREPROCESS, CONV, DWCONV, CHANNEL_MEAN, SE_FC, MAXPOOL = 1, 2, 3, 4, 5, 6, 7
 SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX_CLASS_NMS = 8, 9, 10, 11, 12, 13, 14
-FORK, JOIN = 15, 16
+FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
@@ -159,12 +159,90 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     return y
 
 
-def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None):
+def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None, se_part=False):
+    """Depthwise conv (+ folded BN + act) on NHWC.  With se_part=True it runs the fused variant that
+    also returns the SqueezeExcitation partial channel sums [B, SE_PARTS, C]."""
     _need_cuda(x, w_taps, bias)
     B, H, W, C = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty((B, Ho, Wo, C), dtype=torch.float32, device=x.device)
-    check(lib().edgedet_dwconv2d(_ptr(x), B, H, W, C, _ptr(w_taps), _ptr(bias), k, stride, pad, ACT[act], _ptr(y),
-                                 stream_handle()))
-    return y
+    if not se_part:
+        check(lib().edgedet_dwconv2d(_ptr(x), B, H, W, C, _ptr(w_taps), _ptr(bias), k, stride, pad, ACT[act],
+                                     _ptr(y), stream_handle()))
+        return y
+    part = torch.empty((B, SE_PARTS, C), dtype=torch.float32, device=x.device)
+    rec = np.zeros(1, dtype=OP_DTYPE)
+    rec[0]["kind"] = DWCONV
+    rec[0]["i"][:10] = [B, H, W, C, Ho, Wo, k, stride, pad, ACT[act]]
+    for j, t in enumerate((x, w_taps, bias, y, part)):
+        rec[0]["p"][j] = t.data_ptr()
+    check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
+    return y, part
+
+
+def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ratio=None, path="image"):
+    """SSD.postprocess_detections tail on device buffers (per class score > t, top-k, batched NMS,
+    [:dets]); scores_t [B, NC, A] class probabilities, boxes [B, A, 4] decoded + clipped.
+
+    path="image" runs the SSD_POSTPROCESS record, path="class" the SSD_CLASS_NMS + MERGE_TOPK pair.
+    Returns (out_box [B, dets, 4] scaled by ratio [B, 2], out_score, out_label, out_count)."""
+    _need_cuda(scores_t, boxes, ratio)
+    B, NC, A = scores_t.shape
+    dev = scores_t.device
+    ob = torch.zeros((B, dets, 4), dtype=torch.float32, device=dev)
+    osc = torch.zeros((B, dets), dtype=torch.float32, device=dev)
+    olab = torch.zeros((B, dets), dtype=torch.int64, device=dev)
+    ocnt = torch.zeros((B,), dtype=torch.int32, device=dev)
+    keep_alive = []
+    if path == "image":
+        pk = torch.empty((B, NC - 1, topk), dtype=torch.int32, device=dev)
+        pr = torch.empty((B, NC - 1, topk), dtype=torch.int32, device=dev)
+        rec = np.zeros(1, dtype=OP_DTYPE)
+        rec[0]["kind"] = SSD_POSTPROCESS
+        rec[0]["i"][:5] = [B, A, NC, topk, dets]
+        for j, t in enumerate((scores_t, boxes, pk, pr, ratio, ob, osc, olab, ocnt)):
+            rec[0]["p"][j] = 0 if t is None else t.data_ptr()
+        rec[0]["f"][0] = score_thresh
+        rec[0]["d"][0] = iou_threshold
+        keep_alive += [pk, pr]
+    else:
+        NS = NC - 1
+        rb = torch.empty((B, NS, topk, 4), dtype=torch.float32, device=dev)
+        rs = torch.empty((B, NS, topk), dtype=torch.float32, device=dev)
+        rt = torch.empty((B, NS, topk), dtype=torch.int32, device=dev)
+        rl = torch.empty((B, NS, topk), dtype=torch.int32, device=dev)
+        rc = torch.empty((B, NS), dtype=torch.int32, device=dev)
+        rec = np.zeros(2, dtype=OP_DTYPE)
+        rec[0]["kind"] = SSD_CLASS_NMS
+        rec[0]["i"][:5] = [B, A, NC, topk, topk]
+        for j, t in enumerate((scores_t, boxes, rb, rs, rt, rl, rc)):
+            rec[0]["p"][j] = t.data_ptr()
+        rec[0]["f"][0] = score_thresh
+        rec[0]["d"][0] = iou_threshold
+        rec[1]["kind"] = MERGE_TOPK
+        rec[1]["i"][:4] = [B, NS, topk, dets]
+        for j, t in enumerate((rb, rs, rt, rl, rc, ratio, ob, osc, olab, ocnt)):
+            rec[1]["p"][j] = 0 if t is None else t.data_ptr()
+        keep_alive += [rb, rs, rt, rl, rc]
+    check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), len(rec), stream_handle()))
+    torch.cuda.current_stream().synchronize()
+    return ob, osc, olab, ocnt
+
+
+def se_excitation(part, hw, w1, b1, w2t, b2):
+    """SqueezeExcitation avgpool -> fc1 -> ReLU -> fc2 -> Hardsigmoid from the squeeze partial sums
+    part [B, SE_PARTS, C] over hw pixels; w1 [S, C], w2t [S, C] (fc2 weight transposed).
+    Returns the channel scales [B, C]."""
+    _need_cuda(part, w1, b1, w2t, b2)
+    B, _, C = part.shape
+    S = int(w1.shape[0])
+    scale = torch.empty((B, C), dtype=torch.float32, device=part.device)
+    hidden = torch.empty((B, S), dtype=torch.float32, device=part.device)
+    rec = np.zeros(1, dtype=OP_DTYPE)
+    rec[0]["kind"] = SE_FC
+    rec[0]["i"][:4] = [B, C, S, hw]
+    for j, t in enumerate((part, w1, b1, w2t, b2, scale, hidden)):
+        rec[0]["p"][j] = t.data_ptr()
+    check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
+    return scale

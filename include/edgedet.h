@@ -62,7 +62,8 @@ enum {
     EDGEDET_OP_BOX_SCORES = 13,   /* RoIHeads softmax + class-specific decode + clip                 */
     EDGEDET_OP_BOX_CLASS_NMS = 14,/* per (image, class): score>t, remove_small, NMS                   */
     EDGEDET_OP_FORK = 15,         /* side lanes 1..i[0] wait for everything issued so far on lane 0    */
-    EDGEDET_OP_JOIN = 16          /* lane 0 waits for everything issued so far on lanes 1..i[0]        */
+    EDGEDET_OP_JOIN = 16,         /* lane 0 waits for everything issued so far on lanes 1..i[0]        */
+    EDGEDET_OP_SSD_POSTPROCESS = 17 /* per image: class top-k pool, global-order greedy NMS, [:N]      */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,

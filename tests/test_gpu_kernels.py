@@ -77,7 +77,10 @@ def test_conv_direct_pointwise(case, tile, se):
 
 
 @pytest.mark.parametrize("B,H,W,C,k,s,act", [(2, 20, 20, 72, 5, 2, "RE"), (3, 10, 10, 672, 5, 1, "HS"),
-                                              (2, 3, 3, 128, 3, 2, "R6"), (1, 40, 40, 64, 3, 1, "RE")])
+                                              (2, 3, 3, 128, 3, 2, "R6"), (1, 40, 40, 64, 3, 1, "RE"),
+                                              (2, 13, 7, 16, 3, 2, "RE"), (1, 1, 1, 480, 3, 2, "HS"),
+                                              (2, 9, 11, 40, 5, 2, "HS"), (1, 160, 160, 16, 3, 1, "RE"),
+                                              (2, 6, 9, 8, 3, 1, None), (1, 7, 5, 12, 7, 2, "RE")])
 def test_dwconv_matches_torch(B, H, W, C, k, s, act):
     from edgeml_amd import ops
     from edgeml_amd.plan import pack_dw_weight
@@ -90,6 +93,45 @@ def test_dwconv_matches_torch(B, H, W, C, k, s, act):
                             b.to(DEV), k, s, (k - 1) // 2, act)
     err = (out.permute(0, 3, 1, 2).cpu() - ref).abs().max().item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("B,H,W,C,k,s,act", [(2, 40, 40, 72, 5, 2, "RE"), (3, 10, 10, 672, 5, 1, "HS"),
+                                              (2, 20, 20, 120, 5, 1, "RE"), (1, 5, 5, 960, 5, 1, "HS"),
+                                              (2, 13, 7, 40, 3, 2, "HS"), (1, 2, 2, 24, 5, 1, "RE"),
+                                              (33, 3, 3, 8, 7, 1, "RE")])
+def test_dwconv_se_partial_sums(B, H, W, C, k, s, act):
+    """Fused depthwise + SE squeeze: the output matches torch and the partial sums add up to the
+    per-channel spatial sum of that output."""
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_dw_weight
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(C, 1, k, k, generator=g) / k
+    b = torch.randn(C, generator=g) * 0.1
+    ref = _act(F.conv2d(x, w, b, s, (k - 1) // 2, 1, C), act)
+    y, part = ops.dwconv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV),
+                                torch.from_numpy(pack_dw_weight(w.numpy())).to(DEV), b.to(DEV), k, s, (k - 1) // 2,
+                                act, se_part=True)
+    assert (y.permute(0, 3, 1, 2).cpu() - ref).abs().max().item() < 1e-5
+    tot = part.sum(1).cpu()
+    assert torch.allclose(tot, ref.sum((2, 3)), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,C,S", [(1, 72, 24), (32, 960, 240), (7, 120, 32), (64, 672, 168), (33, 480, 120)])
+def test_se_excitation_matches_torch(B, C, S):
+    """SE avgpool (from SE_PARTS partial sums) -> fc1 -> ReLU -> fc2 -> Hardsigmoid against torch fp32."""
+    from edgeml_amd import ops
+    g = torch.Generator().manual_seed(B + C)
+    hw = 37
+    part = torch.randn(B, ops.SE_PARTS, C, generator=g) * 3
+    w1 = torch.randn(S, C, generator=g) / C ** 0.5
+    b1 = torch.randn(S, generator=g) * 0.1
+    w2 = torch.randn(C, S, generator=g) / S ** 0.5
+    b2 = torch.randn(C, generator=g) * 0.1
+    mean = part.sum(1) / hw
+    ref = F.hardsigmoid(F.linear(F.relu(F.linear(mean, w1, b1)), w2, b2))
+    got = ops.se_excitation(part.to(DEV), hw, w1.to(DEV), b1.to(DEV), w2.t().contiguous().to(DEV), b2.to(DEV))
+    assert (got.cpu() - ref).abs().max().item() < 1e-5
 
 
 def _rand_boxes(rs, n, scale=100.0):

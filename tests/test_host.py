@@ -141,8 +141,13 @@ def test_ssd_plan_lowering():
     m = models.ssdlite320_mobilenet_v3_large()
     P = m.build_plan(4, 640, 480)
     kinds = [op.kind for op in P.ops]
-    assert kinds[0] == ops.PREPROCESS and kinds[-1] == ops.MERGE_TOPK
+    assert kinds[0] == ops.PREPROCESS and kinds[-1] == ops.SSD_POSTPROCESS
     assert kinds.count(ops.FORK) == kinds.count(ops.JOIN) == 1
+    pp = P.ops[-1]
+    assert [pp.i[k] for k in range(5)] == [4, 3234, 91, 300, 300] and 90 * 300 <= m.IMAGE_POOL_MAX
+    m.postprocess = "class"  # the per-class path stays available (pool too large for registers)
+    kinds_c = [op.kind for op in m.build_plan(4, 640, 480).ops]
+    assert kinds_c[-2:] == [ops.SSD_CLASS_NMS, ops.MERGE_TOPK]
     lanes = {op.lane for op in P.ops}
     assert lanes == {0, 1, 2, 3}
     # convs: stem 1 + blocks 0-11 (block 0 has no expansion: 1 + 11*2) + C4 split 2 + blocks 13-14 (2*2)
