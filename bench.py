@@ -99,7 +99,7 @@ def op_work(op):
     if k == O.CHANNEL_MEAN:
         return "se_squeeze", float(i[0] * i[1] * i[2]), 4.0 * i[0] * i[1] * i[2]
     if k == O.SE_FC:
-        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * (2 * i[1] * i[2] + i[0] * (O.SE_PARTS + 1) * i[1] + 2 * i[0] * i[2])
+        return "se_fc", 4.0 * i[0] * i[1] * i[2], 4.0 * (2 * i[1] * i[2] + i[0] * ((i[4] or O.SE_PARTS) + 1) * i[1] + 2 * i[0] * i[2])
     if k == O.MAXPOOL:
         B, H, W, C, Ho, Wo = (i[j] for j in range(6))
         return "maxpool", 0.0, 4.0 * (B * H * W * C + B * Ho * Wo * C)

@@ -284,12 +284,74 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
 
 // ---------------------------------------------------------------------------------------------
 // Pointwise (1x1, stride 1, dense NHWC) conv with operands loaded straight from global memory into
-// MFMA fragments: no LDS, no barriers, four independent waves per block.  For these layers K is small
-// (the narrow MobileNetV3/ResNet 1x1s) and the kernel is bound by HBM, so latency is hidden by wave
-// occupancy instead of LDS staging.  A wave owns a (32*TM) x (32*TN) output tile; lane l supplies
+// MFMA fragments: no LDS, no barriers.  A wave owns a (32*TM) x (32*TN) output tile; lane l supplies
 // row/column (l & 31) and k = 16*(l >> 5) + t of each 32-deep K chunk (t = MFMA step), which for a
-// K-contiguous row is one 64-byte run per lane (a 32-row x 128-byte contiguous block per wave
-// instruction group when Cin == 32).
+// K-contiguous row is one 64-byte run per lane.  The next chunk's fragments are loaded into a
+// second register set before the current chunk's MFMAs issue (one chunk of prefetch), so the
+// memory latency of chunk k+1 overlaps the 16*TM*TN MFMAs of chunk k.
+//
+// pw_splitk_kernel: the same fragments, but the four waves of a workgroup share one 32 x (32*TN)
+// output tile and take every fourth K chunk; their partial tiles are summed through LDS in fixed
+// wave order before the epilogue.  For narrow outputs over long K (SSDLite regression heads and
+// late projections: N <= 96, K >= 256) this gives 4x more waves per tile and 4x shorter chains.
+template <int TM, int TN>
+struct PwFrag {
+    f32x4 a[TM][4], b[TN][4];
+};
+
+template <int TM, int TN>
+__device__ __forceinline__ void pw_load(const ConvParams& p, PwFrag<TM, TN>& f, const float* const (&arow)[TM],
+                                        const int (&ab)[TM], const bool (&aval)[TM], const float* const (&brow)[TN],
+                                        const bool (&bval)[TN], int kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = kk + 4 * q;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (aval[i] && k < p.K) {
+                v = *reinterpret_cast<const f32x4*>(arow[i] + k);
+                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)ab[i] * p.Cin + k);
+            }
+            f.a[i][q] = v;
+        }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            f.b[j][q] = bval[j] ? *reinterpret_cast<const f32x4*>(brow[j] + kk + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void pw_mma(const PwFrag<TM, TN>& f, floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][t >> 2][t & 3], f.b[j][t >> 2][t & 3],
+                                                                  acc[i][j], 0, 0, 0);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void pw_rows(const ConvParams& p, int m0, int n0, int l32, const float* (&arow)[TM],
+                                        int (&ab)[TM], bool (&aval)[TM], const float* (&brow)[TN], bool (&bval)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + i * 32 + l32;
+        aval[i] = m < p.M;
+        arow[i] = p.x + (int64_t)(aval[i] ? m : 0) * p.x_pstride;
+        ab[i] = (p.in_scale && aval[i]) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 32 + l32;
+        bval[j] = n < p.Cout;
+        brow[j] = p.w + (int64_t)(bval[j] ? n : 0) * p.Kpad;
+    }
+}
+
 template <int TM, int TN>
 __global__ void __launch_bounds__(256) pw_mfma_kernel(ConvParams p) {
     const int lane = threadIdx.x & 63;
@@ -304,21 +366,9 @@ __global__ void __launch_bounds__(256) pw_mfma_kernel(ConvParams p) {
     const float* arow[TM];
     int ab[TM];
     bool aval[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int m = m0 + i * 32 + l32;
-        aval[i] = m < p.M;
-        arow[i] = p.x + (int64_t)(aval[i] ? m : 0) * p.x_pstride;
-        ab[i] = (p.in_scale && aval[i]) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
-    }
     const float* brow[TN];
     bool bval[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + j * 32 + l32;
-        bval[j] = n < p.Cout;
-        brow[j] = p.w + (int64_t)(bval[j] ? n : 0) * p.Kpad;
-    }
+    pw_rows<TM, TN>(p, m0, n0, l32, arow, ab, aval, brow, bval);
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -327,36 +377,56 @@ __global__ void __launch_bounds__(256) pw_mfma_kernel(ConvParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    PwFrag<TM, TN> cur, nxt;
+    pw_load<TM, TN>(p, nxt, arow, ab, aval, brow, bval, 16 * h);
     for (int k0 = 0; k0 < p.Kpad; k0 += 32) {
-        const int kk = k0 + 16 * h;
-        f32x4 a[TM][4], b[TN][4];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = kk + 4 * q;
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (aval[i] && k < p.K) {
-                    v = *reinterpret_cast<const f32x4*>(arow[i] + k);
-                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)ab[i] * p.Cin + k);
-                }
-                a[i][q] = v;
-            }
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                b[j][q] = bval[j] ? *reinterpret_cast<const f32x4*>(brow[j] + kk + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][t >> 2][t & 3], b[j][t >> 2][t & 3],
-                                                                      acc[i][j], 0, 0, 0);
+        cur = nxt;
+        if (k0 + 32 < p.Kpad) pw_load<TM, TN>(p, nxt, arow, ab, aval, brow, bval, k0 + 32 + 16 * h);
+        pw_mma<TM, TN>(cur, acc);
     }
     conv_epilogue<TM, TN>(p, acc, m0, n0, h, l32);
+}
+
+template <int TN>
+__global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
+    __shared__ floatx16 red[3][TN][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int nnt = (p.Cout + 32 * TN - 1) / (32 * TN);
+    const int mt = blockIdx.x / nnt, nt = blockIdx.x % nnt;
+    const int m0 = mt * 32, n0 = nt * 32 * TN;
+
+    const float* arow[1];
+    int ab[1];
+    bool aval[1];
+    const float* brow[TN];
+    bool bval[TN];
+    pw_rows<1, TN>(p, m0, n0, l32, arow, ab, aval, brow, bval);
+    floatx16 acc[1][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.f;
+    const int nk = p.Kpad / 32;
+    PwFrag<1, TN> cur, nxt;
+    if (w < nk) pw_load<1, TN>(p, nxt, arow, ab, aval, brow, bval, w * 32 + 16 * h);
+    for (int ks = w; ks < nk; ks += 4) {
+        cur = nxt;
+        if (ks + 4 < nk) pw_load<1, TN>(p, nxt, arow, ab, aval, brow, bval, (ks + 4) * 32 + 16 * h);
+        pw_mma<1, TN>(cur, acc);
+    }
+    if (w > 0)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) red[w - 1][j][lane] = acc[0][j];
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const floatx16 r0 = red[0][j][lane], r1 = red[1][j][lane], r2 = red[2][j][lane];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][j][r] = ((acc[0][j][r] + r0[r]) + r1[r]) + r2[r];
+    }
+    conv_epilogue<1, TN>(p, acc, m0, n0, h, l32);
 }
 
 template <int TM, int TN>
@@ -364,6 +434,15 @@ static int launch_pw(const ConvParams& p, hipStream_t s) {
     const int64_t waves = cdiv(p.M, 32 * TM) * cdiv(p.Cout, 32 * TN);
     EDGEDET_REQUIRE(waves < (1ll << 31), "pw conv grid too large");
     hipLaunchKernelGGL((pw_mfma_kernel<TM, TN>), dim3((unsigned)cdiv(waves, 4)), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int TN>
+static int launch_pw_splitk(const ConvParams& p, hipStream_t s) {
+    const int64_t nwg = cdiv(p.M, 32) * cdiv(p.Cout, 32 * TN);
+    EDGEDET_REQUIRE(nwg < (1ll << 31), "pw conv grid too large");
+    hipLaunchKernelGGL((pw_splitk_kernel<TN>), dim3((unsigned)nwg), dim3(256), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -390,8 +469,9 @@ static int big_tile_override() {
 
 static int choose_tile(const ConvParams& p) {
     if (big_tile_override() && (int64_t)p.M >= 65536 && p.Cout >= 128 && p.Kpad >= 512) return big_tile_override();
+    if (p.lin_x && p.Kpad >= 256 && p.Cout <= 96) return p.Cout <= 32 ? 13 : (p.Cout <= 64 ? 14 : 13);
     if (p.lin_x && (p.Kpad <= 128 || p.Cout <= 32)) {
-        if (p.Cout <= 32) return 11;
+        if (p.Cout <= 32) return 15;
         const int64_t w22 = cdiv(p.M, 64) * cdiv(p.Cout, 64);
         return w22 >= 4 * 256 ? 10 : 12;
     }
@@ -444,6 +524,15 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 12:
             EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
             return launch_pw<1, 2>(p, s);               // direct, 32 x 64 per wave
+        case 15:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw<2, 1>(p, s);               // direct, 64 x 32 per wave
+        case 13:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw_splitk<1>(p, s);           // split-K over 4 waves, 32 x 32
+        case 14:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw_splitk<2>(p, s);           // split-K over 4 waves, 32 x 64
         default: EDGEDET_REQUIRE(false, "conv: unknown tile config");
     }
 }

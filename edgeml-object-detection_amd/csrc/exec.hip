@@ -13,10 +13,10 @@
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
-//                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act
+//                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16)
 //   CHANNEL_MEAN   p0 x[B,HW,C]; p1 mean[B,C]; i0..2 B,HW,C
 //   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; p6 hidden[B,S];
-//                  i0..3 B,C,S,HW
+//                  i0..4 B,C,S,HW,splits (0 = 16)
 //   MAXPOOL        p0 x; p1 y; i0..8 B,H,W,C,Ho,Wo,K,stride,pad
 //   SSD_SCORES     p0 logits[B,A,NC]; p1 reg[B,A,4]; p2 anchors[A,4]; p3 scores_t[B,NC,A];
 //                  p4 boxes[B,A,4]; i0..2 B,A,NC; f0,f1 img_h,img_w
@@ -138,6 +138,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.stride = (int)I[7];
             p.pad = (int)I[8];
             p.act = (int)I[9];
+            p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
             return dwconv_launch(p, s);
         }
         case EDGEDET_OP_CHANNEL_MEAN:
@@ -145,7 +146,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
         case EDGEDET_OP_SE_FC:
             return se_fc_launch(P<const float>(o, 0), P<const float>(o, 1), P<const float>(o, 2), P<const float>(o, 3),
                                 P<const float>(o, 4), P<float>(o, 6), P<float>(o, 5), (int)I[0], (int)I[1], (int)I[2],
-                                (int)I[3], s);
+                                (int)I[3], I[4] > 0 ? (int)I[4] : SE_PARTS, s);
         case EDGEDET_OP_MAXPOOL: {
             PoolParams p{};
             p.x = P<const float>(o, 0);

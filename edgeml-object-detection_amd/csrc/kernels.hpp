@@ -36,8 +36,9 @@ struct DwParams {
     const float* w;  // [K*K][C]
     const float* bias;
     float* y;        // [B][Ho][Wo][C]
-    float* part;     // optional SE squeeze partial sums [B][SE_PARTS][C]
+    float* part;     // optional SE squeeze partial sums [B][parts][C]
     int B, H, W, C, Ho, Wo, K, stride, pad, act;
+    int parts;       // pixel splits of the squeeze (1..SE_PARTS)
 };
 
 struct PoolParams {
@@ -124,7 +125,7 @@ int preprocess_launch(const PreParams& p, hipStream_t s);
 int dwconv_launch(const DwParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);
 int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
-                 float* hidden, float* scale, int B, int C, int S, int HW, hipStream_t s);
+                 float* hidden, float* scale, int B, int C, int S, int HW, int parts, hipStream_t s);
 int maxpool_launch(const PoolParams& p, hipStream_t s);
 int roi_align_launch(const RoiParams& p, hipStream_t s);
 int ssd_scores_launch(const float* logits, const float* reg, const float* anchors, float* scores_t, float* boxes,

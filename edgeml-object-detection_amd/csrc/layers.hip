@@ -100,7 +100,8 @@ __global__ void dwconv_kernel(DwParams p) {
 }
 
 // Depthwise conv + folded BN + act that also emits the SqueezeExcitation squeeze: partial channel
-// sums part[b][s][c] over pixel split s (SE_PARTS splits, reduced in fixed order by se_fc1_kernel).
+// sums part[b][s][c] over pixel split s (p.parts <= SE_PARTS splits, reduced in fixed order by
+// se_fc1_kernel).
 // grid (cdiv(C, 64), SE_PARTS, B); block 256 = 16 channel quads x 16 pixel lanes, so one wave
 // writes 4 pixels x 256 contiguous bytes.
 __global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
     const int c = blockIdx.x * 64 + cq * 4;
     const int sidx = blockIdx.y, b = blockIdx.z;
     const int HWo = p.Ho * p.Wo;
-    const int p0 = (int)((int64_t)sidx * HWo / SE_PARTS), p1 = (int)((int64_t)(sidx + 1) * HWo / SE_PARTS);
+    const int p0 = (int)((int64_t)sidx * HWo / p.parts), p1 = (int)((int64_t)(sidx + 1) * HWo / p.parts);
     f32x4 sum = {0.f, 0.f, 0.f, 0.f};
     if (c < p.C) {
         const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
@@ -146,7 +147,7 @@ __global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
     if (pl == 0 && c < p.C) {
         f32x4 t = red[0][cq];
         for (int q = 1; q < 16; ++q) t += red[q][cq];
-        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * SE_PARTS + sidx) * p.C + c) = t;
+        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * p.parts + sidx) * p.C + c) = t;
     }
 }
 
@@ -228,7 +229,7 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
     const int c = q * 4;
     const int sidx = blockIdx.y, b = blockIdx.z;
     const int G = p.Ho * nwg;
-    const int g0 = (int)((int64_t)sidx * G / SE_PARTS), g1 = (int)((int64_t)(sidx + 1) * G / SE_PARTS);
+    const int g0 = (int)((int64_t)sidx * G / p.parts), g1 = (int)((int64_t)(sidx + 1) * G / p.parts);
     f32x4 sum = {0.f, 0.f, 0.f, 0.f};
     if (q < nq) {
         const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
     if (gl == 0 && q < nq) {
         f32x4 t = red[0][ql];
         for (int k = 1; k < 16; ++k) t += red[k][ql];
-        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * SE_PARTS + sidx) * p.C + c) = t;
+        *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * p.parts + sidx) * p.C + c) = t;
     }
 }
 
@@ -267,7 +268,7 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
     constexpr int PW = 4;
     const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
     if (p.part) {
-        hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW>), dim3((unsigned)cdiv(nq, 16), SE_PARTS, p.B), dim3(256), 0,
+        hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW>), dim3((unsigned)cdiv(nq, 16), p.parts, p.B), dim3(256), 0,
                            s, p, nq, nwg);
     } else {
         const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
@@ -281,12 +282,13 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
 int dwconv_launch(const DwParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
+    if (p.part) EDGEDET_REQUIRE(p.parts >= 1 && p.parts <= SE_PARTS, "dwconv: 1..16 SE partial sums");
     if (p.K == 3 && p.stride == 1) return dwconv_rb_launch<3, 1>(p, s);
     if (p.K == 3 && p.stride == 2) return dwconv_rb_launch<3, 2>(p, s);
     if (p.K == 5 && p.stride == 1) return dwconv_rb_launch<5, 1>(p, s);
     if (p.K == 5 && p.stride == 2) return dwconv_rb_launch<5, 2>(p, s);
     if (p.part) {
-        hipLaunchKernelGGL(dwconv_se_kernel, dim3((unsigned)cdiv(p.C, 64), SE_PARTS, p.B), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(dwconv_se_kernel, dim3((unsigned)cdiv(p.C, 64), p.parts, p.B), dim3(256), 0, s, p);
         EDGEDET_LAUNCH_CHECK();
         return 0;
     }
@@ -337,7 +339,7 @@ constexpr int SE_CMAX = 1024, SE_SMAX = 512;
 
 __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ part, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, float* __restrict__ hidden, int B,
-                                                     int C, int S, int HW) {
+                                                     int C, int S, int HW, int parts) {
     __shared__ float ms[SE1_BB * SE_CMAX];
     __shared__ float ws[SE1_SB * SE_CMAX];
     const int s0 = blockIdx.x * SE1_SB, b0 = blockIdx.y * SE1_BB;
@@ -345,13 +347,13 @@ __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ p
     const float inv = 1.f / (float)HW;
     for (int t = threadIdx.x; t < nb * C; t += 256) {
         const int bl = t / C, c = t - bl * C;
-        const float* pp = part + ((int64_t)(b0 + bl) * SE_PARTS) * C + c;
+        const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
         float v[SE_PARTS];
 #pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)k * C];
+        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)(k < parts ? k : parts - 1) * C];  // independent loads
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) acc += v[k];
+        for (int k = 0; k < SE_PARTS; ++k) acc += k < parts ? v[k] : 0.f;
         ms[t] = acc * inv;
     }
     for (int t = threadIdx.x; t < ns * C; t += 256) ws[t] = w1[(int64_t)s0 * C + t];
@@ -409,11 +411,12 @@ __global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ h
 }
 
 int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
-                 float* hidden, float* scale, int B, int C, int S, int HW, hipStream_t s) {
+                 float* hidden, float* scale, int B, int C, int S, int HW, int parts, hipStream_t s) {
+    EDGEDET_REQUIRE(parts >= 1 && parts <= SE_PARTS, "se_fc: 1..16 squeeze partial sums");
     EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
     EDGEDET_REQUIRE(S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX && HW >= 1, "se_fc: C <= 1024, S <= 512");
     hipLaunchKernelGGL(se_fc1_kernel, dim3((unsigned)cdiv(S, SE1_SB), (unsigned)cdiv(B, SE1_BB)), dim3(256), 0, s,
-                       part, w1, b1, hidden, B, C, S, HW);
+                       part, w1, b1, hidden, B, C, S, HW, parts);
     EDGEDET_LAUNCH_CHECK();
     hipLaunchKernelGGL(se_fc2_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(B, SE2_BB)), dim3(256), 0, s,
                        hidden, w2t, b2, scale, B, C, S);

@@ -218,19 +218,20 @@ class SSDLite320(_Detector):
             Wo = (xs[2] + 2 * pad - k) // stride + 1
             ys = (B, Ho, Wo, xs[3])
             y = P.buf(ys, name=prefix)
-            part = P.buf((B, ops.SE_PARTS, xs[3]), name=prefix + ".se_partial_sums") if se_part else None
+            parts = ops.se_parts(Ho, Wo)
+            part = P.buf((B, parts, xs[3]), name=prefix + ".se_partial_sums") if se_part else None
             P.add(Op(ops.DWCONV, {0: B, 1: xs[1], 2: xs[2], 3: xs[3], 4: Ho, 5: Wo, 6: k, 7: stride, 8: pad,
-                                  9: ops.ACT[act]}, {0: xb, 1: w, 2: b, 3: y, 4: part}, name=prefix))
-            return (y, ys, part) if se_part else (y, ys)
+                                  9: ops.ACT[act], 10: parts}, {0: xb, 1: w, 2: b, 3: y, 4: part}, name=prefix))
+            return (y, ys, (part, parts)) if se_part else (y, ys)
 
         def se(cur, p):
             """SqueezeExcitation excitation from the partial sums the depthwise conv emitted."""
-            xb, xs, part = cur
+            xb, xs, (part, parts) = cur
             w1, b1, w2t, b2, sq = self._se(p)
             C = xs[3]
             scale = P.buf((B, C), name=p + ".scale")
             hidden = P.buf((B, sq), name=p + ".hidden")
-            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: xs[1] * xs[2]},
+            P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: xs[1] * xs[2], 4: parts},
                      {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale, 6: hidden}, name=p))
             return scale
 

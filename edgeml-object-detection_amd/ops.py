@@ -22,7 +22,14 @@ SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX
 FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
 LANE_FIELD, MAX_LANES = 47, 4
 
-SE_PARTS = 16  # pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
+SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
+
+
+def se_parts(ho, wo):
+    """Pixel splits of a fused depthwise+squeeze layer: enough workgroups per image on large maps,
+    and few partial sums to re-read on small ones (>= 16 four-pixel groups per split)."""
+    groups = ho * ((wo + 3) // 4)
+    return max(1, min(SE_PARTS, groups // 16))
 
 # activations (csrc/common.hpp)
 ACT = {None: 0, "RE": 1, "R6": 2, "HS": 3, "HSIG": 4, "SIG": 5}
@@ -161,7 +168,7 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
 
 def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None, se_part=False):
     """Depthwise conv (+ folded BN + act) on NHWC.  With se_part=True it runs the fused variant that
-    also returns the SqueezeExcitation partial channel sums [B, SE_PARTS, C]."""
+    also returns the SqueezeExcitation partial channel sums [B, se_parts(Ho, Wo), C]."""
     _need_cuda(x, w_taps, bias)
     B, H, W, C = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
@@ -171,10 +178,11 @@ def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None, se_part=False):
         check(lib().edgedet_dwconv2d(_ptr(x), B, H, W, C, _ptr(w_taps), _ptr(bias), k, stride, pad, ACT[act],
                                      _ptr(y), stream_handle()))
         return y
-    part = torch.empty((B, SE_PARTS, C), dtype=torch.float32, device=x.device)
+    parts = se_parts(Ho, Wo)
+    part = torch.empty((B, parts, C), dtype=torch.float32, device=x.device)
     rec = np.zeros(1, dtype=OP_DTYPE)
     rec[0]["kind"] = DWCONV
-    rec[0]["i"][:10] = [B, H, W, C, Ho, Wo, k, stride, pad, ACT[act]]
+    rec[0]["i"][:11] = [B, H, W, C, Ho, Wo, k, stride, pad, ACT[act], parts]
     for j, t in enumerate((x, w_taps, bias, y, part)):
         rec[0]["p"][j] = t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
@@ -232,16 +240,16 @@ def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ra
 
 def se_excitation(part, hw, w1, b1, w2t, b2):
     """SqueezeExcitation avgpool -> fc1 -> ReLU -> fc2 -> Hardsigmoid from the squeeze partial sums
-    part [B, SE_PARTS, C] over hw pixels; w1 [S, C], w2t [S, C] (fc2 weight transposed).
+    part [B, splits, C] over hw pixels; w1 [S, C], w2t [S, C] (fc2 weight transposed).
     Returns the channel scales [B, C]."""
     _need_cuda(part, w1, b1, w2t, b2)
-    B, _, C = part.shape
+    B, parts, C = part.shape
     S = int(w1.shape[0])
     scale = torch.empty((B, C), dtype=torch.float32, device=part.device)
     hidden = torch.empty((B, S), dtype=torch.float32, device=part.device)
     rec = np.zeros(1, dtype=OP_DTYPE)
     rec[0]["kind"] = SE_FC
-    rec[0]["i"][:4] = [B, C, S, hw]
+    rec[0]["i"][:5] = [B, C, S, hw, parts]
     for j, t in enumerate((part, w1, b1, w2t, b2, scale, hidden)):
         rec[0]["p"][j] = t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))

@@ -67,10 +67,12 @@ def test_conv_every_lds_tile(case, tile):
     _conv_case(*case, tile=tile)
 
 
-@pytest.mark.parametrize("tile", [10, 11, 12])
+@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("case", [(2, 20, 20, 112, 672, 1, 1, "HS", False), (3, 10, 10, 40, 120, 1, 1, None, True),
                                   (2, 33, 31, 24, 72, 1, 1, "RE", False), (1, 9, 9, 16, 16, 1, 1, None, True),
-                                  (2, 13, 11, 96, 24, 1, 1, "R6", False)])
+                                  (2, 13, 11, 96, 24, 1, 1, "R6", False), (2, 20, 20, 672, 24, 1, 1, None, False),
+                                  (3, 10, 10, 480, 80, 1, 1, None, True), (2, 5, 5, 512, 546, 1, 1, None, False),
+                                  (1, 3, 3, 1000, 36, 1, 1, "HS", False)])
 @pytest.mark.parametrize("se", [False, True])
 def test_conv_direct_pointwise(case, tile, se):
     _conv_case(*case, tile=tile, se=se)
@@ -117,13 +119,14 @@ def test_dwconv_se_partial_sums(B, H, W, C, k, s, act):
     assert torch.allclose(tot, ref.sum((2, 3)), rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("B,C,S", [(1, 72, 24), (32, 960, 240), (7, 120, 32), (64, 672, 168), (33, 480, 120)])
-def test_se_excitation_matches_torch(B, C, S):
-    """SE avgpool (from SE_PARTS partial sums) -> fc1 -> ReLU -> fc2 -> Hardsigmoid against torch fp32."""
+@pytest.mark.parametrize("B,C,S,parts", [(1, 72, 24, 16), (32, 960, 240, 1), (7, 120, 32, 5), (64, 672, 168, 2),
+                                          (33, 480, 120, 16)])
+def test_se_excitation_matches_torch(B, C, S, parts):
+    """SE avgpool (from `parts` partial sums) -> fc1 -> ReLU -> fc2 -> Hardsigmoid against torch fp32."""
     from edgeml_amd import ops
     g = torch.Generator().manual_seed(B + C)
     hw = 37
-    part = torch.randn(B, ops.SE_PARTS, C, generator=g) * 3
+    part = torch.randn(B, parts, C, generator=g) * 3
     w1 = torch.randn(S, C, generator=g) / C ** 0.5
     b1 = torch.randn(S, generator=g) * 0.1
     w2 = torch.randn(C, S, generator=g) / S ** 0.5
