@@ -67,13 +67,35 @@ def timed_steps(plan, stream, steps, warmup, dist):
 
 
 # ------------------------------------------------------------------------------ per-op costs
-def conv_grid(op):
-    """(workgroups, threads per workgroup) of a CONV op, as csrc/conv.hip picks its tile."""
+BF16X6_PEAK_TFS = 157.3 * 16 / 6  # dense bf16 MFMA (16x the fp32 rate) / six partial products
+
+CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads (0 BM = waves of 64-row pw)
+    1: ("conv_mfma_kernel", 128, 32, 256), 2: ("conv_mfma_kernel", 128, 64, 256),
+    3: ("conv_mfma_kernel", 128, 128, 256), 4: ("conv_mfma_kernel", 256, 128, 512),
+    5: ("conv_mfma_kernel", 64, 64, 256), 6: ("conv_mfma_kernel", 32, 32, 64),
+    10: ("pw_mfma_kernel", 256, 64, 256), 11: ("pw_mfma_kernel", 512, 32, 256), 12: ("pw_mfma_kernel", 128, 64, 256),
+    15: ("pw_mfma_kernel", 256, 32, 256), 13: ("pw_splitk_kernel", 32, 32, 256), 14: ("pw_splitk_kernel", 32, 64, 256),
+    22: ("conv_x6_kernel", 128, 64, 256), 23: ("conv_x6_kernel", 128, 128, 256), 24: ("conv_x6_kernel", 256, 128, 512),
+}
+
+
+def conv_tile(op_record):
+    """The kernel variant libedgedet runs for this CONV record (edgedet_conv_tile)."""
+    import ctypes
+    from edgeml_amd import ops as O
+    t = O.lib().edgedet_conv_tile(op_record.ctypes.data_as(ctypes.c_void_p))
+    if t < 0:
+        O.check(t)
+    return t
+
+
+def conv_grid(op, rec):
+    """(kernel name, workgroups, threads per workgroup, fp32-equivalent MFMA peak) of a CONV record."""
     i = op.i
     M, Cout = i[0] * i[4] * i[5], i[6]
-    tile = i[23] or (1 if Cout <= 32 else (2 if Cout <= 64 else 3))
-    bm, bn, nt = {1: (128, 32, 256), 2: (128, 64, 256), 3: (128, 128, 256), 4: (256, 128, 512)}[tile]
-    return -(-M // bm) * -(-Cout // bn), nt
+    name, bm, bn, nt = CONV_TILES[conv_tile(rec)]
+    wg = -(-M // bm) * -(-Cout // bn)
+    return name, wg, nt, (BF16X6_PEAK_TFS if name == "conv_x6_kernel" else FP32_MFMA_PEAK_TFS)
 
 
 def op_work(op):
@@ -123,6 +145,8 @@ def op_work(op):
         return "box_scores", 0.0, 4.0 * i[1] * i[2] * (i[0] + 5 * i[3])
     if k == O.BOX_CLASS_NMS:
         return "class_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 5
+    if k in (O.FORK, O.JOIN):
+        return "lanes", 0.0, 0.0
     return f"kind{k}", 0.0, 0.0
 
 
@@ -161,27 +185,37 @@ def roofline_for(plan, stream, step_ms, model=""):
     """Dominant kernel family of the step (by measured device time) and its longest launch, priced
     against the roof that binds it (max of flops / fp32-MFMA peak and bytes / HBM peak)."""
     times = per_op_times(plan, stream)
+    from edgeml_amd import ops as O
     OP_DUMP[model] = [{"name": op.name, "family": op_work(op)[0], "ms": round(t, 5), "flops": op_work(op)[1],
-                       "bytes": op_work(op)[2]} for op, t in zip(plan.ops, times)]
+                       "bytes": op_work(op)[2],
+                       "tile": conv_tile(plan.records[k:k + 1]) if op.kind == O.CONV else None}
+                      for k, (op, t) in enumerate(zip(plan.ops, times))]
     fam = {}
     for op, t in zip(plan.ops, times):
         name = op_work(op)[0]
-        fam[name] = fam.get(name, 0.0) + t
+        if name != "lanes":
+            fam[name] = fam.get(name, 0.0) + t
     dom = max(fam, key=fam.get)
     op, t = max(((o, t) for o, t in zip(plan.ops, times) if op_work(o)[0] == dom), key=lambda x: x[1])
     name, flops, byts = op_work(op)
-    t_f = flops / (FP32_MFMA_PEAK_TFS * 1e12)
+    kname, peak_tf = {"dwconv": "dwconv_kernel"}.get(name, name), FP32_MFMA_PEAK_TFS
+    k = plan.ops.index(op)
+    if name == "conv":
+        kname, wg, nt, peak_tf = conv_grid(op, plan.records[k:k + 1])
+    t_f = flops / (peak_tf * 1e12)
     t_b = byts / (HBM_PEAK_GBS * 1e9)
-    out = {"kernel": {"conv": "conv_mfma_kernel", "dwconv": "dwconv_kernel"}.get(name, name), "launch": op.name,
+    out = {"kernel": kname, "launch": op.name,
            "launch_ms": round(t, 4), "algorithmic_flops": flops, "algorithmic_bytes": byts,
            "family_ms": {k: round(v, 4) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
            "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
     if name == "conv":
-        out["grid_wg"], out["wg_threads"] = conv_grid(op)
+        out["grid_wg"], out["wg_threads"] = wg, nt
+        if kname == "conv_x6_kernel":
+            out["peak_basis"] = "dense bf16 MFMA 2516.6 TFLOP/s / 6 bf16 products per fp32 product"
     if t_f >= t_b:
         ach = flops / (t * 1e-3) / 1e12
-        out.update({"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": round(ach / FP32_MFMA_PEAK_TFS, 4)})
+        out.update({"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak_tf, 1), "unit": "TFLOP/s",
+                    "frac": round(ach / peak_tf, 4)})
     else:
         ach = byts / (t * 1e-3) / 1e9
         out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -248,6 +282,7 @@ def main():
 
     dist, rank, world = dist_setup(args.gpus)
     from edgeml_amd import models, synthetic
+    from edgeml_amd import plan as plan_mod
     stream = torch.cuda.Stream()
     out = {}
     if args.model in ("ssd", "both"):
@@ -298,6 +333,7 @@ def main():
         "config": {"workload": "ssdlite320_mobilenet_v3_large b=%d 640x640 (configs[1])" % p["batch"]
                    if primary == "ssd" else "fasterrcnn_resnet50_fpn_v2 b=%d 640x640 (configs[2])" % p["batch"],
                    "global_batch": p["batch"] * world, "parallelism": f"dp{world}",
+                   "conv_math": plan_mod.CONV_MATH,
                    "weights": "seeded synthetic (COCO weights need a download)"},
     }
     if "frcnn" in out and primary == "ssd":

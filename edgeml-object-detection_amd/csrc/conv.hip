@@ -429,6 +429,237 @@ __global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
     conv_epilogue<1, TN>(p, acc, m0, n0, h, l32);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM through the bf16 matrix cores: the six-term split ("bf16x6").
+//
+// gfx950 issues v_mfma_f32_32x32x16_bf16 at 16x the rate of v_mfma_f32_32x32x2_f32.  Every fp32
+// operand is split exactly into three bf16 terms x = x0 + x1 + x2 (x0 = RN_bf16(x),
+// x1 = RN_bf16(x - x0), x2 = x - x0 - x1, which fits bf16 exactly: 24 = 3 x 8 significant bits), and
+// the product is accumulated from the six partial products whose magnitude is at or above
+// 2^-24 |a b|:  a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0.  The three dropped terms are bounded by
+// (2^-9 * 2^-18) * 3 < 2^-24 |a b|, below one fp32 rounding of the product, and every kept bf16 x bf16
+// product is exact in the fp32 accumulator.  Six bf16 MFMAs (6 x 32 cycles) replace eight f32
+// MFMAs (8 x 64 cycles) per 32x32x16 block: 2.67x the fp32-MFMA rate at fp32-grade accuracy.
+//
+// Weights arrive pre-split as three bf16 planes w3[3][Cout][Kpad] (plan.py split_bf16x3; the same
+// RN split); activations are split once per block while staging (global fp32 -> registers ->
+// three bf16 planes in LDS), so the split costs O(BM*K) VALU per block, not O(BM*BN*K).
+// LDS: K stage of 16, rows of 16 bf16 padded to 24 (48 B: the 16-lane b128 read groups hit 16
+// disjoint 4-bank groups), double-buffered through registers, one barrier per stage.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK6 = 16;
+constexpr int LDR6 = 24;  // padded LDS row, in bf16
+
+__device__ __forceinline__ void split3_bf16(const f32x4& v, u16x4& h, u16x4& m, u16x4& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e];
+        const __bf16 x0 = (__bf16)x;
+        const float r1 = x - (float)x0;
+        const __bf16 x1 = (__bf16)r1;
+        const float r2 = r1 - (float)x1;
+        const __bf16 x2 = (__bf16)r2;
+        h[e] = __builtin_bit_cast(unsigned short, x0);
+        m[e] = __builtin_bit_cast(unsigned short, x1);
+        l[e] = __builtin_bit_cast(unsigned short, x2);
+    }
+}
+
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
+    constexpr int NT = WM * WN * 64;
+    constexpr int BM = WM * TM * 32;
+    constexpr int BN = WN * TN * 32;
+    constexpr int AJ = BM * 4 / NT;      // f32x4 A loads per thread per stage
+    constexpr int BL = 3 * BN * 2;             // 16-B B-plane loads per stage
+    constexpr int BJ = (BL + NT - 1) / NT;     // ... per thread
+    static_assert(AJ >= 1 && BM * 4 == AJ * NT, "tile too small for block");
+    constexpr int PA = BM * LDR6, PB = BN * LDR6;  // one plane of one buffer (bf16 elements)
+
+    __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * (PA + PB)];
+    unsigned short* As = lds;                 // [buf][plane][BM][LDR6]
+    unsigned short* Bs = lds + 2 * 3 * PA;    // [buf][plane][BN][LDR6]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wave_m = wid / WN;
+    const int wave_n = wid % WN;
+
+    const int nmt = (p.M + BM - 1) / BM;
+    const int nnt = (p.Cout + BN - 1) / BN;
+    const int nwg = nmt * nnt;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int mt = bid / nnt;
+    const int nt = bid % nnt;
+    const int m0 = mt * BM;
+    const int n0 = nt * BN;
+
+    const int c4 = tid & 3;  // f32x4 column within the 16-wide stage
+    int64_t a_base[AJ];
+    int a_ih0[AJ], a_iw0[AJ], a_b[AJ];
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+        const int row = (tid >> 2) + (NT / 4) * j;
+        const int m = m0 + row;
+        if (m < p.M && p.lin_x) {
+            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_base[j] = (int64_t)m * p.x_pstride;
+            a_ih0[j] = 0;
+            a_iw0[j] = 0;
+        } else if (m < p.M) {
+            const int b = (int)fdiv((uint32_t)m, p.div_howo);
+            const int rem = m - b * p.Ho * p.Wo;
+            const int oh = (int)fdiv((uint32_t)rem, p.div_wo);
+            const int ow = rem - oh * p.Wo;
+            a_b[j] = b;
+            a_base[j] = (int64_t)b * p.x_bstride;
+            a_ih0[j] = oh * p.stride - p.pad;
+            a_iw0[j] = ow * p.stride - p.pad;
+        } else {
+            a_b[j] = 0;
+            a_base[j] = 0;
+            a_ih0[j] = -(1 << 28);
+            a_iw0[j] = 0;
+        }
+    }
+    const int KHW = p.KH * p.KW;
+    const int64_t wplane = (int64_t)p.Cout * p.Kpad;
+    const unsigned short* w3 = reinterpret_cast<const unsigned short*>(p.w3);
+
+    f32x4 ra[AJ];
+    uint4 rb[BJ];
+
+    auto load_stage = [&](int k0) {
+        const int k = k0 + c4 * 4;
+        const int tap = (int)fdiv((uint32_t)k, p.div_cin);
+        const int ci = k - tap * p.Cin;
+        const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+        const int kw = tap - kh * p.KW;
+        const bool kval = tap < KHW;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
+                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+            }
+            ra[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int lin = tid + NT * j;
+            const int half = lin & 1, row = (lin >> 1) % BN, pl = (lin >> 1) / BN;
+            const int n = n0 + row;
+            uint4 v = uint4{0u, 0u, 0u, 0u};
+            if ((BL % NT == 0 || lin < BL) && n < p.Cout) v = *reinterpret_cast<const uint4*>(w3 + pl * wplane + (int64_t)n * p.Kpad + k0 + 8 * half);
+            rb[j] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        unsigned short* A = As + buf * 3 * PA;
+        unsigned short* Bb = Bs + buf * 3 * PB;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int row = (tid >> 2) + (NT / 4) * j;
+            u16x4 h, m, l;
+            split3_bf16(ra[j], h, m, l);
+            *reinterpret_cast<u16x4*>(A + 0 * PA + row * LDR6 + c4 * 4) = h;
+            *reinterpret_cast<u16x4*>(A + 1 * PA + row * LDR6 + c4 * 4) = m;
+            *reinterpret_cast<u16x4*>(A + 2 * PA + row * LDR6 + c4 * 4) = l;
+        }
+#pragma unroll
+        for (int j = 0; j < BJ; ++j) {
+            const int lin = tid + NT * j;
+            const int half = lin & 1, row = (lin >> 1) % BN, pl = (lin >> 1) / BN;
+            if (BL % NT == 0 || lin < BL) *reinterpret_cast<uint4*>(Bb + pl * PB + row * LDR6 + 8 * half) = rb[j];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = p.Kpad / BK6;
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) load_stage((kc + 1) * BK6);
+        const unsigned short* A = As + buf * 3 * PA;
+        const unsigned short* Bb = Bs + buf * 3 * PB;
+        bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                af[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * PA + (wave_m * TM * 32 + i * 32 + l32) * LDR6 + 8 * h);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + (wave_n * TN * 32 + j * 32 + l32) * LDR6 + 8 * h);
+        // smallest terms first: (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
+            }
+        if (kc + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+
+    conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+}
+
+// Device-side weight split (the same RN three-term split as plan.py split_bf16x3): w[n] fp32 ->
+// out[3][n] bf16 planes.
+__global__ void split_bf16x3_kernel(const float* __restrict__ w, int64_t n, unsigned short* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = w[i];
+    const __bf16 x0 = (__bf16)x;
+    const float r1 = x - (float)x0;
+    const __bf16 x1 = (__bf16)r1;
+    const __bf16 x2 = (__bf16)(r1 - (float)x1);
+    out[i] = __builtin_bit_cast(unsigned short, x0);
+    out[n + i] = __builtin_bit_cast(unsigned short, x1);
+    out[2 * n + i] = __builtin_bit_cast(unsigned short, x2);
+}
+
+template <int WM, int WN, int TM, int TN>
+static int launch_x6(const ConvParams& p, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
+    EDGEDET_REQUIRE(p.Kpad % BK6 == 0, "conv bf16x6: Kpad must be a multiple of 16");
+    const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, BN);
+    EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
+    hipLaunchKernelGGL((conv_x6_kernel<WM, WN, TM, TN>), dim3((unsigned)nwg), dim3(WM * WN * 64), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
 template <int TM, int TN>
 static int launch_pw(const ConvParams& p, hipStream_t s) {
     const int64_t waves = cdiv(p.M, 32 * TM) * cdiv(p.Cout, 32 * TN);
@@ -486,8 +717,8 @@ static int choose_tile(const ConvParams& p) {
     return c[nc - 1].tile;
 }
 
-// Host launcher shared by the plan executor and the unit C entry point.
-int conv_launch(ConvParams p, int tile, hipStream_t s) {
+// Validation and the derived fields (fast divisors, dense-layout flags) of a conv problem.
+int conv_prepare(ConvParams& p) {
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "conv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.Cin % 4 == 0, "conv: Cin must be a multiple of 4 (pad channels)");
     EDGEDET_REQUIRE(p.x_pstride % 4 == 0, "conv: input pixel stride must be a multiple of 4");
@@ -507,8 +738,28 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
                p.x_bstride == (int64_t)p.H * p.W * p.x_pstride) ? 1 : 0;
     p.lin_y = (p.y_bstride == (int64_t)p.Ho * p.Wo * p.y_pstride) ? 1 : 0;
     p.lin_res = (p.res_H == p.Ho && p.res_W == p.Wo && p.res_bstride == (int64_t)p.Ho * p.Wo * p.res_pstride) ? 1 : 0;
-    if (tile <= 0) tile = choose_tile(p);
+    return 0;
+}
+
+// The kernel variant that runs: the requested tile, or the automatic choice (compute-bound LDS
+// tiles switch to their bf16x6 form when the split weight planes are present).
+int conv_resolve_tile(const ConvParams& p, int tile) {
+    if (tile <= 0) {
+        tile = choose_tile(p);
+        if (p.w3 && tile >= 2 && tile <= 4) tile += 20;
+    }
+    return tile;
+}
+
+// Host launcher shared by the plan executor and the unit C entry point.
+int conv_launch(ConvParams p, int tile, hipStream_t s) {
+    const int rc = conv_prepare(p);
+    if (rc) return rc;
+    tile = conv_resolve_tile(p, tile);
     switch (tile) {
+        case 22: return launch_x6<2, 2, 2, 1>(p, s);  // 128 x 64, bf16x6
+        case 23: return launch_x6<2, 2, 2, 2>(p, s);  // 128 x 128, bf16x6
+        case 24: return launch_x6<4, 2, 2, 2>(p, s);  // 256 x 128, bf16x6
         case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
         case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
         case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128
@@ -545,10 +796,20 @@ extern "C" int64_t edgedet_conv_weight_k(int32_t KH, int32_t KW, int64_t Cin) {
     return cdiv((int64_t)KH * KW * Cin, BK) * BK;
 }
 
-extern "C" int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
-                              const float* bias, int64_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                              int32_t pad, int32_t act, const float* res, float* y, void* stream) {
+extern "C" int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream) {
+    EDGEDET_REQUIRE(w && out && n > 0, "split_bf16x3: null pointer or empty");
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, w, n,
+                       reinterpret_cast<unsigned short*>(out));
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                                 const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH, int32_t KW,
+                                 int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
+                                 void* stream) {
     ConvParams p{};
+    p.w3 = w3;
     p.x = x;
     p.w = w;
     p.bias = bias;
@@ -575,5 +836,11 @@ extern "C" int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, i
     p.y_bstride = (int64_t)p.Ho * p.Wo * Cout;
     p.res_pstride = (int)Cout;
     p.res_bstride = p.y_bstride;
-    return conv_launch(p, 0, (hipStream_t)stream);
+    return conv_launch(p, tile, (hipStream_t)stream);
+}
+
+extern "C" int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                              const float* bias, int64_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                              int32_t pad, int32_t act, const float* res, float* y, void* stream) {
+    return edgedet_conv2d_ex(x, B, H, W, Cin, w, nullptr, bias, Cout, KH, KW, stride, pad, act, res, y, 0, stream);
 }

@@ -8,7 +8,7 @@
 // Record layouts (i = int64 fields, p = device pointers, d = doubles, f = floats):
 //   MEMSET         p0 ptr; i0 bytes
 //   PREPROCESS     p0 x[B,3,H,W]; p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
-//   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0;
+//   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0; p6 w3 bf16 planes|0;
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
@@ -63,6 +63,44 @@ static SegOut seg_out(const edgedet_op& o, int k0, int kmax) {
     return s;
 }
 
+// CONV record -> ConvParams (layout in the header comment above).
+static ConvParams conv_params(const edgedet_op& o) {
+    const int64_t* I = o.i;
+    ConvParams p{};
+    p.x = P<const float>(o, 0);
+    p.w = P<const float>(o, 1);
+    p.bias = P<const float>(o, 2);
+    p.y = P<float>(o, 3);
+    p.res = P<const float>(o, 4);
+    p.in_scale = P<const float>(o, 5);
+    p.w3 = P<const void>(o, 6);
+    p.B = (int)I[0];
+    p.H = (int)I[1];
+    p.W = (int)I[2];
+    p.Cin = (int)I[3];
+    p.Ho = (int)I[4];
+    p.Wo = (int)I[5];
+    p.Cout = (int)I[6];
+    p.KH = (int)I[7];
+    p.KW = (int)I[8];
+    p.stride = (int)I[9];
+    p.pad = (int)I[10];
+    p.act = (int)I[11];
+    p.K = (int)I[12];
+    p.Kpad = (int)I[13];
+    p.x_pstride = (int)I[14];
+    p.y_pstride = (int)I[15];
+    p.res_pstride = (int)I[16];
+    p.x_bstride = I[17];
+    p.y_bstride = I[18];
+    p.res_bstride = I[19];
+    p.y_off = I[20];
+    p.res_H = (int)I[21];
+    p.res_W = (int)I[22];
+    p.M = p.B * p.Ho * p.Wo;
+    return p;
+}
+
 static int run_op(const edgedet_op& o, hipStream_t s) {
     const int64_t* I = o.i;
     switch (o.kind) {
@@ -87,37 +125,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             return preprocess_launch(p, s);
         }
         case EDGEDET_OP_CONV: {
-            ConvParams p{};
-            p.x = P<const float>(o, 0);
-            p.w = P<const float>(o, 1);
-            p.bias = P<const float>(o, 2);
-            p.y = P<float>(o, 3);
-            p.res = P<const float>(o, 4);
-            p.in_scale = P<const float>(o, 5);
-            p.B = (int)I[0];
-            p.H = (int)I[1];
-            p.W = (int)I[2];
-            p.Cin = (int)I[3];
-            p.Ho = (int)I[4];
-            p.Wo = (int)I[5];
-            p.Cout = (int)I[6];
-            p.KH = (int)I[7];
-            p.KW = (int)I[8];
-            p.stride = (int)I[9];
-            p.pad = (int)I[10];
-            p.act = (int)I[11];
-            p.K = (int)I[12];
-            p.Kpad = (int)I[13];
-            p.x_pstride = (int)I[14];
-            p.y_pstride = (int)I[15];
-            p.res_pstride = (int)I[16];
-            p.x_bstride = I[17];
-            p.y_bstride = I[18];
-            p.res_bstride = I[19];
-            p.y_off = I[20];
-            p.res_H = (int)I[21];
-            p.res_W = (int)I[22];
-            p.M = p.B * p.Ho * p.Wo;
+            const ConvParams p = conv_params(o);
             EDGEDET_REQUIRE(p.K == p.KH * p.KW * p.Cin, "conv: K != KH*KW*Cin");
             return conv_launch(p, (int)I[23], s);
         }
@@ -380,6 +388,15 @@ extern "C" int edgedet_graph_destroy(void* graph) {
     if (g->graph) (void)hipGraphDestroy(g->graph);
     delete g;
     return 0;
+}
+
+// The conv kernel variant (tile id, csrc/conv.hip conv_launch) a CONV record runs, without launching.
+extern "C" int edgedet_conv_tile(const edgedet_op* op) {
+    EDGEDET_REQUIRE(op && op->kind == EDGEDET_OP_CONV, "conv_tile: not a CONV record");
+    ConvParams p = conv_params(*op);
+    const int rc = conv_prepare(p);
+    if (rc) return rc;
+    return conv_resolve_tile(p, (int)op->i[23]);
 }
 
 extern "C" const char* edgedet_last_error(void) { return get_error(); }

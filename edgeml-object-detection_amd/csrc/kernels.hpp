@@ -13,6 +13,7 @@ struct ConvParams {
     float* y;
     const float* res;
     const float* in_scale;  // [B][Cin] or null (SE excitation)
+    const void* w3;         // bf16 split planes [3][Cout][Kpad] or null (bf16x6 tiles)
     int B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, act;
     int K, Kpad, M;
     int x_pstride, y_pstride, res_pstride;
@@ -120,6 +121,8 @@ struct SsdPostParams {
     double iou;
 };
 
+int conv_prepare(ConvParams& p);
+int conv_resolve_tile(const ConvParams& p, int tile);
 int conv_launch(ConvParams p, int tile, hipStream_t s);
 int preprocess_launch(const PreParams& p, hipStream_t s);
 int dwconv_launch(const DwParams& p, hipStream_t s);

@@ -17,7 +17,7 @@ import torch
 from . import anchors as anc
 from . import arch
 from . import ops
-from .plan import Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight
+from .plan import Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight, split_bf16x3
 
 
 def _np(t):
@@ -90,7 +90,7 @@ class _Detector:
                 self._w[key] = (self.pack.add(pack_dw_weight(wf)), self.pack.add(bf), wf.shape[-1], None, wf.shape[0])
             else:
                 wp, K, Kpad, cin = pack_conv_weight(wf, cin_pad)
-                self._w[key] = (self.pack.add(wp), self.pack.add(bf), K, Kpad, cin)
+                self._w[key] = (self._conv_w(wp), self.pack.add(bf), K, Kpad, cin)
         return self._w[key]
 
     def _conv_bias(self, wkey, bkey, perm=None):
@@ -101,11 +101,17 @@ class _Detector:
             if w.ndim == 2:
                 w = w[:, :, None, None]
             wp, K, Kpad, cin = pack_conv_weight(w)
-            self._w[key] = (self.pack.add(wp), self.pack.add(b), K, Kpad, cin)
+            self._w[key] = (self._conv_w(wp), self.pack.add(b), K, Kpad, cin)
         return self._w[key]
 
     def _is_dw(self, wkey):
         return False
+
+    def _conv_w(self, wp):
+        """Pack a [Cout][Kpad] conv weight plus its three bf16 planes (the bf16x6 tiles' operand)."""
+        ref = self.pack.add(wp)
+        ref.split = self.pack.add_u16(split_bf16x3(wp))
+        return ref
 
     # inference --------------------------------------------------------------------------------
     def plan(self, B, H, W):
@@ -356,7 +362,7 @@ class FasterRCNNFPNv2(_Detector):
             w = w.reshape(-1, 256, 7, 7).transpose(0, 2, 3, 1).reshape(w.shape[0], -1)  # -> (h, w, c)
             b = _np(self.sd["roi_heads.box_head.5.bias"]).astype(np.float32)
             wp, K, Kpad, cin = pack_conv_weight(w[:, :, None, None])
-            self._w[key] = (self.pack.add(wp), self.pack.add(b), K, Kpad, cin)
+            self._w[key] = (self._conv_w(wp), self.pack.add(b), K, Kpad, cin)
         return self._w[key]
 
     def _predictor(self):
@@ -366,7 +372,7 @@ class FasterRCNNFPNv2(_Detector):
             w = np.concatenate([_np(self.sd[q + "bbox_pred.weight"]), _np(self.sd[q + "cls_score.weight"])], 0)
             b = np.concatenate([_np(self.sd[q + "bbox_pred.bias"]), _np(self.sd[q + "cls_score.bias"])], 0)
             wp, K, Kpad, cin = pack_conv_weight(w.astype(np.float32)[:, :, None, None])
-            self._w[key] = (self.pack.add(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
+            self._w[key] = (self._conv_w(wp), self.pack.add(b.astype(np.float32)), K, Kpad, cin)
         return self._w[key]
 
 

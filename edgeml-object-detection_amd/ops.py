@@ -40,7 +40,8 @@ assert OP_DTYPE.itemsize == 8 + 8 * OP_INTS + 8 * OP_PTRS + 8 * OP_DBLS + 4 * OP
 
 EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
-           "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target")
+           "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
+           "edgedet_split_bf16x3", "edgedet_conv_tile")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -77,6 +78,11 @@ def lib():
     L.edgedet_roi_align.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _flt, _i32, _i32, _i32, _vp, _vp]
     L.edgedet_conv2d.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                                  _vp, _vp]
+    L.edgedet_conv2d_ex.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
+                                    _vp, _vp, _i32, _vp]
+    L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
+    L.edgedet_conv_tile.argtypes = [_vp]
+    L.edgedet_conv_tile.restype = ctypes.c_int
     L.edgedet_conv_weight_k.argtypes = [_i32, _i32, _i64]
     L.edgedet_conv_weight_k.restype = _i64
     L.edgedet_dwconv2d.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]
@@ -84,7 +90,7 @@ def lib():
     L.edgedet_version.restype = _i32
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
-                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d"):
+                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L
@@ -138,20 +144,34 @@ def roi_align_nhwc(feat_nhwc, rois, spatial_scale, output_size=7, sampling_ratio
     return out
 
 
-def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, tile=0, in_scale=None):
+def split_bf16x3(w):
+    """Device split of an fp32 tensor into three bf16 planes (uint16 bit patterns, [3, *w.shape]):
+    the weights of the bf16x6 conv tiles (edgedet_split_bf16x3; same split as plan.split_bf16x3)."""
+    _need_cuda(w)
+    out = torch.empty((3,) + tuple(w.shape), dtype=torch.int16, device=w.device)
+    check(lib().edgedet_split_bf16x3(_ptr(w), w.numel(), _ptr(out), stream_handle()))
+    return out
+
+
+def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, tile=0, in_scale=None, w3=None):
     """Fused conv (+ folded BN) + residual + activation on NHWC; w_packed from plan.pack_conv_weight.
 
-    tile=0 goes through the C entry point edgedet_conv2d (automatic tile choice); a non-zero tile
-    (or an SE ``in_scale`` [B, Cin]) runs one CONV plan record so every kernel variant is testable.
+    tile=0 goes through the C entry point edgedet_conv2d_ex (automatic tile choice; with the split
+    weight planes ``w3`` the compute-bound tiles run bf16x6); a non-zero tile (or an SE ``in_scale``
+    [B, Cin]) runs one CONV plan record so every kernel variant is testable.
     """
-    _need_cuda(x, w_packed, bias, res, in_scale)
+    _need_cuda(x, w_packed, bias, res, in_scale, w3)
     B, H, W, Cin = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
     if tile == 0 and in_scale is None:
-        check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad,
-                                   ACT[act], _ptr(res), _ptr(y), stream_handle()))
+        if w3 is None:
+            check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad,
+                                       ACT[act], _ptr(res), _ptr(y), stream_handle()))
+        else:
+            check(lib().edgedet_conv2d_ex(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(w3), _ptr(bias), cout, k, k,
+                                          stride, pad, ACT[act], _ptr(res), _ptr(y), 0, stream_handle()))
         return y
     K = k * k * Cin
     kpad = int(lib().edgedet_conv_weight_k(k, k, Cin))
@@ -160,7 +180,7 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     vals = [B, H, W, Cin, Ho, Wo, cout, k, k, stride, pad, ACT[act], K, kpad, Cin, cout, cout, H * W * Cin,
             Ho * Wo * cout, Ho * Wo * cout, 0, Ho, Wo, tile]
     rec[0]["i"][:len(vals)] = vals
-    for j, t in enumerate((x, w_packed, bias, y, res, in_scale)):
+    for j, t in enumerate((x, w_packed, bias, y, res, in_scale, w3)):
         rec[0]["p"][j] = 0 if t is None else t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
     return y

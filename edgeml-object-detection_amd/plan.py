@@ -11,6 +11,7 @@ A detector forward for a fixed (batch, height, width) is lowered once into
 Nothing here computes detections: every FLOP runs in the HIP kernels of libedgedet.so.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -18,6 +19,32 @@ import torch
 from . import ops
 
 ALIGN = 256
+
+# Conv math of the compute-bound conv tiles: "bf16x6" (fp32 GEMM as six bf16 partial products on the
+# bf16 matrix cores, error below one fp32 rounding per product; csrc/conv.hip) or "f32"
+# (v_mfma_f32_32x32x2_f32).  Override with EDGEDET_CONV_MATH=f32.
+CONV_MATH = os.environ.get("EDGEDET_CONV_MATH", "bf16x6")
+if CONV_MATH not in ("bf16x6", "f32"):
+    raise ValueError(f"EDGEDET_CONV_MATH must be 'bf16x6' or 'f32', got {CONV_MATH!r}")
+
+
+def _bf16_rn(x):
+    """float32 array -> (bf16 bit patterns as uint16, the bf16 values as float32), round to nearest even."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    r = ((u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16)).astype(np.uint32)
+    return r.astype(np.uint16), (r << np.uint32(16)).view(np.float32)
+
+
+def split_bf16x3(w):
+    """fp32 w -> uint16 [3, *w.shape]: x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1) (= exact).
+    The weight operand of the bf16x6 conv tiles (same arithmetic as csrc/conv.hip split3_bf16)."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    h0, f0 = _bf16_rn(w)
+    r1 = (w - f0).astype(np.float32)
+    h1, f1 = _bf16_rn(r1)
+    r2 = (r1 - f1).astype(np.float32)
+    h2, _ = _bf16_rn(r2)
+    return np.stack([h0, h1, h2])
 
 
 # ------------------------------------------------------------------------------ weights
@@ -29,8 +56,18 @@ class WeightPack:
         self.size = 0  # in floats
         self.device_blob = None
 
+    def add_u16(self, arr):
+        """Add a uint16 array (bf16 bit patterns) of even length, stored bit-exact in the float blob."""
+        a = np.ascontiguousarray(arr, dtype=np.uint16).reshape(-1)
+        if a.size % 2:
+            a = np.concatenate([a, np.zeros(1, np.uint16)])
+        return self.add(a.view(np.float32))
+
     def add(self, arr):
-        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32)).reshape(-1)
+        if isinstance(arr, np.ndarray) and arr.dtype == np.float32:
+            a = np.ascontiguousarray(arr).reshape(-1)
+        else:
+            a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32)).reshape(-1)
         off = self.size
         self.arrays.append((off, a))
         self.size = off + ((a.size + 63) // 64) * 64
@@ -49,6 +86,7 @@ class WeightPack:
 class WRef:
     def __init__(self, pack, off, n):
         self.pack, self.off, self.n = pack, off, n
+        self.split = None  # WRef of the bf16x3 planes of a packed conv weight (conv_op p6)
 
     def ptr(self):
         return self.pack.device_blob.data_ptr() + 4 * self.off
@@ -253,4 +291,5 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
          13: Kpad, 14: xp, 15: yp, 16: cout, 17: (H * W * xp if x_bstride is None else x_bstride),
          18: (Ho * Wo * yp if y_bstride is None else y_bstride), 19: rH * rW * cout, 20: y_off, 21: rH, 22: rW,
          23: tile}
-    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale}, name=name))
+    w3 = getattr(w, "split", None) if CONV_MATH == "bf16x6" else None
+    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale, 6: w3}, name=name))

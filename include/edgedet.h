@@ -118,10 +118,27 @@ int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin,
                    int32_t pad, int32_t act, const float* res, float* y, void* stream);
 int64_t edgedet_conv_weight_k(int32_t KH, int32_t KW, int64_t Cin);
 
+/*
+ * edgedet_conv2d with the math selectable: w3 (nullable) holds the packed weight split into three
+ * bf16 planes [3][Cout][Kpad] (edgedet_split_bf16x3).  With w3 the compute-bound tiles run the
+ * fp32 GEMM on the bf16 matrix cores as six partial products (error below one fp32 rounding per
+ * product, csrc/conv.hip "bf16x6"); without it they run v_mfma_f32_32x32x2_f32.  tile 0 = auto.
+ */
+int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                      const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH, int32_t KW,
+                      int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
+                      void* stream);
+/* w [n] fp32 -> out [3][n] bf16 bit patterns: x0 = RN(x), x1 = RN(x - x0), x2 = x - x0 - x1 (exact). */
+int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream);
+
 /* Depthwise conv2d (+ folded BN + act).  x NHWC [B,H,W,C]; w [KH*KW][C]; bias [C]. */
 int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,
                      const float* bias, int32_t K, int32_t stride, int32_t pad, int32_t act,
                      float* y, void* stream);
+
+/* The conv kernel variant (tile id of csrc/conv.hip conv_launch: 1-6 fp32-MFMA LDS tiles, 10-15
+ * direct pointwise tiles, 22-24 bf16x6 LDS tiles) that a CONV record would run; negative on error. */
+int edgedet_conv_tile(const edgedet_op* op);
 
 /* --------------------------------------------------------------------------------- misc */
 const char* edgedet_last_error(void);

@@ -32,7 +32,7 @@ CONV_CASES = [
 ]
 
 
-def _conv_case(B, H, W, Cin, Cout, k, s, act, res, tile=0, se=False):
+def _conv_case(B, H, W, Cin, Cout, k, s, act, res, tile=0, se=False, x6=False):
     from edgeml_amd import ops
     from edgeml_amd.plan import pack_conv_weight
     g = torch.Generator().manual_seed(1)
@@ -48,9 +48,11 @@ def _conv_case(B, H, W, Cin, Cout, k, s, act, res, tile=0, se=False):
         ref = ref + r
     ref = _act(ref, act)
     wp, K, Kpad, _ = pack_conv_weight(w.numpy())
-    out = ops.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), torch.from_numpy(wp).to(DEV), b.to(DEV), Cout,
+    wdev = torch.from_numpy(wp).to(DEV)
+    w3 = ops.split_bf16x3(wdev) if x6 else None
+    out = ops.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), wdev, b.to(DEV), Cout,
                           k, s, pad, act, r.permute(0, 2, 3, 1).contiguous().to(DEV) if res else None, tile=tile,
-                          in_scale=sc.to(DEV) if se else None)
+                          in_scale=sc.to(DEV) if se else None, w3=w3)
     got = out.permute(0, 3, 1, 2).cpu()
     err = (got - ref).abs().max().item()
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
@@ -203,3 +205,47 @@ def test_nms_exact_ratio_boundaries(thr):
     ref = tv_ops.nms(boxes, scores, thr)
     got = ops.nms(torch.from_numpy(boxes).to(DEV), torch.from_numpy(scores).to(DEV), thr).cpu().numpy()
     np.testing.assert_array_equal(got, ref)
+
+
+# ---- bf16x6: the fp32 GEMM as six bf16 partial products (csrc/conv.hip conv_x6_kernel)
+def test_split_bf16x3_device_matches_host():
+    from edgeml_amd import ops
+    from edgeml_amd.plan import split_bf16x3
+    g = torch.Generator().manual_seed(3)
+    w = torch.cat([torch.randn(40000, generator=g) * 10 ** torch.randint(-6, 4, (40000,), generator=g),
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0e38, 1e-38, 65504.0])])
+    got = ops.split_bf16x3(w.to(DEV)).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, split_bf16x3(w.numpy()))
+
+
+@pytest.mark.parametrize("tile", [0, 22, 23, 24])
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 7, 8)])
+def test_conv_bf16x6_matches_torch(case, tile):
+    _conv_case(*case, tile=tile, x6=True)
+
+
+@pytest.mark.parametrize("tile", [22, 23, 24])
+def test_conv_bf16x6_se_scale(tile):
+    _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)
+
+
+@pytest.mark.parametrize("shape", [(2, 25, 25, 256, 256, 3), (1, 13, 13, 1024, 512, 1), (1, 50, 50, 64, 128, 7)])
+def test_conv_bf16x6_is_fp32_grade(shape):
+    """Against a float64 reference the bf16x6 conv errs no more than the exact-fp32 MFMA conv (x1.5):
+    the three dropped partial products sit below one fp32 rounding of each product."""
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight
+    B, H, W, Cin, Cout, k = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.zeros(Cout)
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, (k - 1) // 2)
+    wp = torch.from_numpy(pack_conv_weight(w.numpy())[0]).to(DEV)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    errs = {}
+    for name, w3 in (("f32", None), ("x6", ops.split_bf16x3(wp))):
+        for tile in (23,) if w3 is not None else (3,):
+            y = ops.conv2d_nhwc(xd, wp, b.to(DEV), Cout, k, 1, (k - 1) // 2, None, tile=tile, w3=w3)
+            errs[name] = (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max().item()
+    assert errs["x6"] <= 1.5 * errs["f32"] + 1e-7, errs
