@@ -76,6 +76,7 @@ CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads
     10: ("pw_mfma_kernel", 256, 64, 256), 11: ("pw_mfma_kernel", 512, 32, 256), 12: ("pw_mfma_kernel", 128, 64, 256),
     15: ("pw_mfma_kernel", 256, 32, 256), 13: ("pw_splitk_kernel", 32, 32, 256), 14: ("pw_splitk_kernel", 32, 64, 256),
     22: ("conv_x6_kernel", 128, 64, 256), 23: ("conv_x6_kernel", 128, 128, 256), 24: ("conv_x6_kernel", 256, 128, 512),
+    25: ("conv_x6b_kernel", 256, 128, 512),
 }
 
 
@@ -95,7 +96,7 @@ def conv_grid(op, rec):
     M, Cout = i[0] * i[4] * i[5], i[6]
     name, bm, bn, nt = CONV_TILES[conv_tile(rec)]
     wg = -(-M // bm) * -(-Cout // bn)
-    return name, wg, nt, (BF16X6_PEAK_TFS if name == "conv_x6_kernel" else FP32_MFMA_PEAK_TFS)
+    return name, wg, nt, (BF16X6_PEAK_TFS if name.startswith("conv_x6") else FP32_MFMA_PEAK_TFS)
 
 
 def op_work(op):
@@ -210,7 +211,7 @@ def roofline_for(plan, stream, step_ms, model=""):
            "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
     if name == "conv":
         out["grid_wg"], out["wg_threads"] = wg, nt
-        if kname == "conv_x6_kernel":
+        if kname.startswith("conv_x6"):
             out["peak_basis"] = "dense bf16 MFMA 2516.6 TFLOP/s / 6 bf16 products per fp32 product"
     if t_f >= t_b:
         ach = flops / (t * 1e-3) / 1e12

@@ -449,6 +449,9 @@ __global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
+#ifndef X6_PF
+#define X6_PF 1
+#endif
 constexpr int BK6 = 16;
 constexpr int LDR6 = 24;  // padded LDS row, in bf16
 
@@ -531,46 +534,79 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     }
     const int KHW = p.KH * p.KW;
     const int64_t wplane = (int64_t)p.Cout * p.Kpad;
-    const unsigned short* w3 = reinterpret_cast<const unsigned short*>(p.w3);
-
-    f32x4 ra[AJ];
-    uint4 rb[BJ];
-
-    auto load_stage = [&](int k0) {
-        const int k = k0 + c4 * 4;
-        const int tap = (int)fdiv((uint32_t)k, p.div_cin);
-        const int ci = k - tap * p.Cin;
-        const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
-        const int kw = tap - kh * p.KW;
-        const bool kval = tap < KHW;
+    // Per-thread source pointers, fixed across K stages: the A row at filter tap (0, 0) (only
+    // dereferenced when in bounds) and the B-plane row.
+    const float* a_row[AJ];
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
-            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
-                v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
-            }
-            ra[j] = v;
-        }
+    for (int j = 0; j < AJ; ++j) a_row[j] = p.x + a_base[j] + ((int64_t)a_ih0[j] * p.W + a_iw0[j]) * p.x_pstride;
+    const unsigned short* b_row[BJ];
+    bool b_ok[BJ];
 #pragma unroll
-        for (int j = 0; j < BJ; ++j) {
-            const int lin = tid + NT * j;
-            const int half = lin & 1, row = (lin >> 1) % BN, pl = (lin >> 1) / BN;
-            const int n = n0 + row;
-            uint4 v = uint4{0u, 0u, 0u, 0u};
-            if ((BL % NT == 0 || lin < BL) && n < p.Cout) v = *reinterpret_cast<const uint4*>(w3 + pl * wplane + (int64_t)n * p.Kpad + k0 + 8 * half);
-            rb[j] = v;
-        }
+    for (int j = 0; j < BJ; ++j) {
+        const int lin = tid + NT * j;
+        const int half = lin & 1, row = (lin >> 1) % BN, pl = (lin >> 1) / BN;
+        const int n = n0 + row;
+        b_ok[j] = (BL % NT == 0 || lin < BL) && n < p.Cout;
+        b_row[j] = reinterpret_cast<const unsigned short*>(p.w3) + pl * wplane + (int64_t)(b_ok[j] ? n : 0) * p.Kpad +
+                   8 * half;
+    }
+    // Cin % 16 == 0: a 16-wide K stage never crosses a filter tap, so the tap of a stage is
+    // wavefront-uniform (scalar) and a thread's A address is its row pointer plus a uniform offset.
+    const bool uniform_tap = (p.Cin & 15) == 0;
+
+    struct Regs {
+        f32x4 a[AJ];
+        uint4 b[BJ];
     };
-    auto store_stage = [&](int buf) {
+    Regs r0, r1;
+
+    auto load_stage = [&](Regs& R, int k0) {
+        if (uniform_tap) {
+            const int tap = (int)fdiv((uint32_t)k0, p.div_cin);
+            const int ci = k0 - tap * p.Cin + c4 * 4;
+            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+            const int kw = tap - kh * p.KW;
+            const bool kval = tap < KHW;
+            const int64_t off = ((int64_t)kh * p.W + kw) * p.x_pstride + ci;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (kval && (unsigned)(a_ih0[j] + kh) < (unsigned)p.H && (unsigned)(a_iw0[j] + kw) < (unsigned)p.W) {
+                    v = *reinterpret_cast<const f32x4*>(a_row[j] + off);
+                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                }
+                R.a[j] = v;
+            }
+        } else {
+            const int k = k0 + c4 * 4;
+            const int tap = (int)fdiv((uint32_t)k, p.div_cin);
+            const int ci = k - tap * p.Cin;
+            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+            const int kw = tap - kh * p.KW;
+            const bool kval = tap < KHW;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                    v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
+                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                }
+                R.a[j] = v;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < BJ; ++j)
+            R.b[j] = b_ok[j] ? *reinterpret_cast<const uint4*>(b_row[j] + k0) : uint4{0u, 0u, 0u, 0u};
+    };
+    auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
 #pragma unroll
         for (int j = 0; j < AJ; ++j) {
             const int row = (tid >> 2) + (NT / 4) * j;
             u16x4 h, m, l;
-            split3_bf16(ra[j], h, m, l);
+            split3_bf16(R.a[j], h, m, l);
             *reinterpret_cast<u16x4*>(A + 0 * PA + row * LDR6 + c4 * 4) = h;
             *reinterpret_cast<u16x4*>(A + 1 * PA + row * LDR6 + c4 * 4) = m;
             *reinterpret_cast<u16x4*>(A + 2 * PA + row * LDR6 + c4 * 4) = l;
@@ -579,7 +615,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
         for (int j = 0; j < BJ; ++j) {
             const int lin = tid + NT * j;
             const int half = lin & 1, row = (lin >> 1) % BN, pl = (lin >> 1) / BN;
-            if (BL % NT == 0 || lin < BL) *reinterpret_cast<uint4*>(Bb + pl * PB + row * LDR6 + 8 * half) = rb[j];
+            if (BL % NT == 0 || lin < BL) *reinterpret_cast<uint4*>(Bb + pl * PB + row * LDR6 + 8 * half) = R.b[j];
         }
     };
 
@@ -592,15 +628,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int nk = p.Kpad / BK6;
-    load_stage(0);
-    store_stage(0);
-    __syncthreads();
-
     const int h = lane >> 5;
     const int l32 = lane & 31;
-    for (int kc = 0; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage((kc + 1) * BK6);
+    auto compute = [&](int buf) {
         const unsigned short* A = As + buf * 3 * PA;
         const unsigned short* Bb = Bs + buf * 3 * PB;
         bf16x8 af[TM][3], bfr[TN][3];
@@ -626,11 +656,245 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
             }
+    };
+#if X6_PF == 2
+    // Two stages of register prefetch: stage k+2's global loads are issued before stage k's MFMAs,
+    // stage k+1 (loaded one step earlier) is split and stored to LDS after them.
+    load_stage(r0, 0);
+    store_stage(r0, 0);
+    __syncthreads();
+    if (nk > 1) load_stage(r0, BK6);
+    auto step = [&](int kc, Regs& hold, Regs& next) {
+        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6);
+        compute(kc & 1);
+        if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
+        __syncthreads();
+    };
+    for (int kc = 0; kc < nk; kc += 2) {
+        step(kc, r0, r1);
+        if (kc + 1 < nk) step(kc + 1, r1, r0);
+    }
+#else
+    load_stage(r0, 0);
+    store_stage(r0, 0);
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6);
+        compute(kc & 1);
+        if (kc + 1 < nk) store_stage(r0, (kc & 1) ^ 1);
+        __syncthreads();
+    }
+#endif
+
+    conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+}
+
+// bf16x6 with a 32-deep K stage: 256 x 128 block tile on 8 waves (4 x 2, 64 x 64 per wave), 48 MFMAs
+// per wave between barriers.  LDS rows are 32 bf16 (64 B) with the 16-B chunks XOR-swizzled by
+// row bits 2..3 (chunk' = chunk ^ ((row >> 2) & 3)): the four lane groups of a ds_read_b128 then hit
+// 16 distinct 16-B slots of the 256-B bank row (conflict-free), and the double-buffered image of the
+// three A and three B planes fits 144 KiB (one block of 8 waves per CU, two waves per SIMD).
+#ifndef X6_T14
+#define X6_T14 0
+#endif
+#ifndef X6_PRIO
+#define X6_PRIO 0
+#endif
+constexpr int BK6B = 32;
+
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
+
+__global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
+    constexpr int WM = 4, WN = 2, TM = 2, TN = 2, NT = 512;
+    constexpr int BM = 256, BN = 128;
+    constexpr int AJ = BM * BK6B / 4 / NT;  // 4 f32x4 A loads per thread per stage
+    constexpr int PA = BM * BK6B, PB = BN * BK6B;  // bf16 elements per plane
+    static_assert(3 * BN * BK6B / 8 == 3 * NT, "one B-plane chunk per thread per plane");
+
+    __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * (PA + PB)];
+    unsigned short* As = lds;
+    unsigned short* Bs = lds + 2 * 3 * PA;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wave_m = wid / WN;
+    const int wave_n = wid % WN;
+
+    const int nmt = (p.M + BM - 1) / BM;
+    const int nnt = (p.Cout + BN - 1) / BN;
+    const int nwg = nmt * nnt;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    }
+    const int m0 = (bid / nnt) * BM;
+    const int n0 = (bid % nnt) * BN;
+
+    const int c8 = tid & 7;  // f32x4 column of the 32-deep stage
+    int64_t a_base[AJ];
+    int a_ih0[AJ], a_iw0[AJ], a_b[AJ];
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+        const int m = m0 + (tid >> 3) + (NT / 8) * j;
+        if (m < p.M && p.lin_x) {
+            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_base[j] = (int64_t)m * p.x_pstride;
+            a_ih0[j] = 0;
+            a_iw0[j] = 0;
+        } else if (m < p.M) {
+            const int b = (int)fdiv((uint32_t)m, p.div_howo);
+            const int rem = m - b * p.Ho * p.Wo;
+            const int oh = (int)fdiv((uint32_t)rem, p.div_wo);
+            const int ow = rem - oh * p.Wo;
+            a_b[j] = b;
+            a_base[j] = (int64_t)b * p.x_bstride;
+            a_ih0[j] = oh * p.stride - p.pad;
+            a_iw0[j] = ow * p.stride - p.pad;
+        } else {
+            a_b[j] = 0;
+            a_base[j] = 0;
+            a_ih0[j] = -(1 << 28);
+            a_iw0[j] = 0;
+        }
+    }
+    const int KHW = p.KH * p.KW;
+    const int64_t wplane = (int64_t)p.Cout * p.Kpad;
+    const int b_row = tid >> 2, b_chunk = tid & 3;
+    const bool b_ok = n0 + b_row < p.Cout;
+    const unsigned short* b_src = reinterpret_cast<const unsigned short*>(p.w3) +
+                                  (int64_t)(b_ok ? n0 + b_row : 0) * p.Kpad + 8 * b_chunk;
+
+    f32x4 ra[AJ];
+    uint4 rb[3];
+    auto load_stage = [&](int k0) {
+        const int k = k0 + c8 * 4;
+        const int tap = (int)fdiv((uint32_t)k, p.div_cin);
+        const int ci = k - tap * p.Cin;
+        const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+        const int kw = tap - kh * p.KW;
+        const bool kval = tap < KHW;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
+                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+            }
+            ra[j] = v;
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            rb[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
+    };
+    auto store_stage = [&](int buf) {
+        unsigned short* A = As + buf * 3 * PA;
+        unsigned short* Bb = Bs + buf * 3 * PB;
+#pragma unroll
+        for (int j = 0; j < AJ; ++j) {
+            const int row = (tid >> 3) + (NT / 8) * j;
+            u16x4 h, m, l;
+            split3_bf16(ra[j], h, m, l);
+            const int o = swz64(row, c8 >> 1) + 4 * (c8 & 1);
+            *reinterpret_cast<u16x4*>(A + 0 * PA + o) = h;
+            *reinterpret_cast<u16x4*>(A + 1 * PA + o) = m;
+            *reinterpret_cast<u16x4*>(A + 2 * PA + o) = l;
+        }
+        const int o = swz64(b_row, b_chunk);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = rb[pl];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = p.Kpad / BK6B;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    auto compute = [&](int buf) {
+        const unsigned short* A = As + buf * 3 * PA;
+        const unsigned short* Bb = Bs + buf * 3 * PB;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int o = swz64(wave_m * TM * 32 + i * 32 + l32, 2 * s + h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * PA + o);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int o = swz64(wave_n * TN * 32 + j * 32 + l32, 2 * s + h);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
+            }
+#if X6_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
+                }
+#if X6_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
+        }
+    };
+#if X6_T14
+    // Write-after-barrier: the registers loaded during stage k-1 are split and stored into the free
+    // buffer at the top of stage k, then stage k+2's loads are issued and stage k's MFMAs run.
+    load_stage(0);
+    store_stage(0);
+    if (nk > 1) load_stage(BK6B);
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) {
+            store_stage(buf ^ 1);
+            if (kc + 2 < nk) load_stage((kc + 2) * BK6B);
+        }
+        compute(buf);
+        __syncthreads();
+    }
+#else
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < nk) load_stage((kc + 1) * BK6B);
+        compute(buf);
         if (kc + 1 < nk) store_stage(buf ^ 1);
         __syncthreads();
     }
+#endif
 
     conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+}
+
+static int launch_x6b(const ConvParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
+    EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
+    const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128);
+    EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
+    hipLaunchKernelGGL(conv_x6b_kernel, dim3((unsigned)nwg), dim3(512), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
 }
 
 // Device-side weight split (the same RN three-term split as plan.py split_bf16x3): w[n] fp32 ->
@@ -746,7 +1010,11 @@ int conv_prepare(ConvParams& p) {
 int conv_resolve_tile(const ConvParams& p, int tile) {
     if (tile <= 0) {
         tile = choose_tile(p);
-        if (p.w3 && tile >= 2 && tile <= 4) tile += 20;
+        if (p.w3 && tile >= 2 && tile <= 4) {
+            tile += 20;
+            // large problems: the 32-deep-stage 256 x 128 tile (>= 2 workgroups per CU)
+            if (tile >= 23 && cdiv(p.M, 256) * cdiv(p.Cout, 128) >= 512) tile = 25;
+        }
     }
     return tile;
 }
@@ -760,6 +1028,7 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 22: return launch_x6<2, 2, 2, 1>(p, s);  // 128 x 64, bf16x6
         case 23: return launch_x6<2, 2, 2, 2>(p, s);  // 128 x 128, bf16x6
         case 24: return launch_x6<4, 2, 2, 2>(p, s);  // 256 x 128, bf16x6
+        case 25: return launch_x6b(p, s);             // 256 x 128, bf16x6, 32-deep swizzled stages
         case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
         case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
         case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128

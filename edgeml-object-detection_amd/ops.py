@@ -12,7 +12,7 @@ import numpy as np
 import torch  # noqa: F401  (must precede loading libedgedet.so: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libedgedet.so")
+LIB_PATH = os.environ.get("EDGEDET_LIB") or os.path.join(HERE, "libedgedet.so")  # override: A/B builds
 
 OP_INTS, OP_PTRS, OP_DBLS, OP_FLTS = 48, 24, 8, 16
 

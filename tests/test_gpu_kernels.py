@@ -218,13 +218,13 @@ def test_split_bf16x3_device_matches_host():
     assert np.array_equal(got, split_bf16x3(w.numpy()))
 
 
-@pytest.mark.parametrize("tile", [0, 22, 23, 24])
+@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25])
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 7, 8)])
 def test_conv_bf16x6_matches_torch(case, tile):
     _conv_case(*case, tile=tile, x6=True)
 
 
-@pytest.mark.parametrize("tile", [22, 23, 24])
+@pytest.mark.parametrize("tile", [22, 23, 24, 25])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)
 
@@ -244,8 +244,9 @@ def test_conv_bf16x6_is_fp32_grade(shape):
     wp = torch.from_numpy(pack_conv_weight(w.numpy())[0]).to(DEV)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     errs = {}
-    for name, w3 in (("f32", None), ("x6", ops.split_bf16x3(wp))):
-        for tile in (23,) if w3 is not None else (3,):
+    for name, w3 in (("f32", None), ("x6", ops.split_bf16x3(wp))):  # keys: f323, x623, x625
+        for tile in (23, 25) if w3 is not None else (3,):
             y = ops.conv2d_nhwc(xd, wp, b.to(DEV), Cout, k, 1, (k - 1) // 2, None, tile=tile, w3=w3)
-            errs[name] = (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max().item()
-    assert errs["x6"] <= 1.5 * errs["f32"] + 1e-7, errs
+            errs[f"{name}{tile}"] = (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max().item()
+    assert errs["x623"] <= 1.5 * errs["f323"] + 1e-7, errs
+    assert errs["x625"] <= 1.5 * errs["f323"] + 1e-7, errs
