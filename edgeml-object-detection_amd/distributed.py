@@ -70,3 +70,24 @@ def gather_rows(results, my_names, all_names, rank, world, device=None):
             out[name] = rr[pos:pos + n].copy().reshape(int(n), 6)
             pos += int(n)
     return out
+
+
+def gather_values(vals, my_idx, n, rank, world, device=None):
+    """Per-image float64 values of this rank's contiguous shard (my_idx) -> the full [n] array on rank 0
+    (reward.py: every rank computes the ORIE of its shard of target images)."""
+    if world == 1:
+        return np.asarray(vals, np.float64)
+    backend = dist.get_backend()
+    dev = device or (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu"))
+    width = max(shard_bounds(n, k, world)[1] - shard_bounds(n, k, world)[0] for k in range(world))
+    buf = torch.zeros(max(width, 1), dtype=torch.float64, device=dev)
+    buf[:len(my_idx)] = torch.from_numpy(np.asarray(vals, np.float64)).to(dev)
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    if rank != 0:
+        return None
+    out = np.zeros(n)
+    for k in range(world):
+        lo, hi = shard_bounds(n, k, world)
+        out[lo:hi] = bufs[k].cpu().numpy()[:hi - lo]
+    return out

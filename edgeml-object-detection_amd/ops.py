@@ -41,7 +41,7 @@ assert OP_DTYPE.itemsize == 8 + 8 * OP_INTS + 8 * OP_PTRS + 8 * OP_DBLS + 4 * OP
 EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
-           "edgedet_split_bf16x3", "edgedet_conv_tile")
+           "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -81,6 +81,8 @@ def lib():
     L.edgedet_conv2d_ex.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
                                     _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
+    L.edgedet_box_correct.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _dbl, _vp, _i64, _vp]
+    L.edgedet_orie_ap.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _vp]
     L.edgedet_conv_tile.argtypes = [_vp]
     L.edgedet_conv_tile.restype = ctypes.c_int
     L.edgedet_conv_weight_k.argtypes = [_i32, _i32, _i64]
@@ -90,7 +92,7 @@ def lib():
     L.edgedet_version.restype = _i32
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
-                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3"):
+                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L

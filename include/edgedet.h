@@ -140,6 +140,29 @@ int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C,
  * direct pointwise tiles, 22-24 bf16x6 LDS tiles) that a CONV record would run; negative on error. */
 int edgedet_conv_tile(const edgedet_op* op);
 
+/* ------------------------------------------------------------------ ORIE consumer (reward.py) */
+/*
+ * lib/metrics.py box_correct (lib/data.py set_data's TP flags) for many images at once: detections
+ * det_xyxy [n_det][4] f64 + det_cls, labels lab_xyxy [n_lab][4] f64 + lab_cls, both grouped per image
+ * by the offsets det_off / lab_off [n_img + 1]; tp [n_det] = 1 where the detection is matched at
+ * IoU >= iou_thr.  max_labels = the most labels of any one image (<= 1024).
+ */
+int edgedet_box_correct(const double* det_xyxy, const int32_t* det_cls, const int64_t* det_off,
+                        const double* lab_xyxy, const int32_t* lab_cls, const int64_t* lab_off,
+                        int64_t n_img, double iou_thr, uint8_t* tp, int64_t max_labels, void* stream);
+/*
+ * reward.py compute_orie's two ap_per_class calls (lib/metrics.py:89-148) for n_eval evaluations.
+ * Entries = every detection of every image (weak and strong), sorted per class by (conf desc, image,
+ * row, weak before strong); ent_img [n_ent], ent_flag [n_ent] (bit0 TP, bit1 strong), class segments
+ * seg_off [n_cls + 1]; lab_cnt [n_img][n_cls] labels per image and class; evaluation e targets image
+ * target[e] with ensemble ens[e][0..E) (target excluded).  ap [n_eval][2][n_cls] (weak, strong AP per
+ * class, float64, bit-identical to numpy's), n_l [n_eval][n_cls] (labels of the class in the ensemble
+ * plus the target; the reference's unique classes are those with n_l > 0).
+ */
+int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off, int32_t n_cls,
+                    const int32_t* lab_cnt, int64_t n_img, const int32_t* target, const int32_t* ens, int32_t E,
+                    int64_t n_eval, double* ap, int32_t* n_l, void* stream);
+
 /* --------------------------------------------------------------------------------- misc */
 const char* edgedet_last_error(void);
 /* Library/ABI version: (major << 16) | minor. */

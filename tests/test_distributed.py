@@ -61,3 +61,29 @@ def test_gather_rows_world2(n):
     assert sorted(got) == names
     for k in names:
         np.testing.assert_array_equal(np.asarray(got[k]).reshape(-1, 6), _rows_for(k))
+
+
+def _values_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from edgeml_amd import distributed as D
+    mine = D.shard(list(range(n)), rank, world)
+    out = D.gather_values(np.asarray(mine, np.float64) * 1.5, mine, n, rank, world)
+    if rank == 0:
+        q.put(out.tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [0, 1, 7])
+def test_gather_values_world2(n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_values_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert got == [1.5 * i for i in range(n)]

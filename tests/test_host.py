@@ -188,3 +188,33 @@ def test_split_bf16x3_is_exact():
     a = np.abs(w.astype(np.float64))
     assert np.all(np.abs(vals[1]) <= a * 2.0 ** -8 * (1 + 1e-7))
     assert np.all(np.abs(vals[2]) <= a * 2.0 ** -16 * (1 + 1e-7))
+
+
+def test_reward_ensembles_are_the_reference_draws():
+    """edgeml_amd.reward.ensembles = reward.py:34-38 under np.random.seed(seed + i) (oracle harness)."""
+    import numpy as np
+    from edgeml_amd import reward
+    for n, e in ((1, 5), (7, 0), (30, 10), (30, 100)):
+        E, ens = reward.ensembles(n, e, seed=3)
+        assert E == min(e, n - 1) and ens.shape == (n, E)
+        for i in range(n):
+            np.random.seed(3 + i)
+            idx = np.arange(n - 1)
+            if i < n - 1:
+                idx[i:] += 1
+            np.testing.assert_array_equal(ens[i], np.random.permutation(idx)[:E])
+            assert i not in ens[i]
+
+
+def test_reward_entries_sorted_by_class_then_conf():
+    import numpy as np
+    from edgeml_amd import reward
+    tp = lambda n: np.zeros((n, 1), bool)  # noqa: E731
+    weak = [(tp(3), np.array([0.2, 0.9, 0.5]), np.array([1, 1, 7])), (tp(0), np.array([]), np.array([]))]
+    strong = [(tp(1), np.array([0.95]), np.array([1])), (tp(2), np.array([0.9, 0.3]), np.array([1, 3]))]
+    labels = [np.array([1, 3]), np.array([])]
+    C, lab_cnt, img, flag, seg = reward._entries(weak, strong, labels)
+    assert C == 2 and seg.tolist() == [0, 4, 5]  # class 7 has no labels: dropped
+    np.testing.assert_array_equal(img, [0, 0, 1, 0, 1])       # conf .95(s), .9(w,img0), .9(s,img1), .2 | 3: .3
+    np.testing.assert_array_equal(flag >> 1, [1, 0, 1, 0, 1])
+    np.testing.assert_array_equal(lab_cnt, [[1, 1], [0, 0]])
