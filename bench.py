@@ -146,6 +146,13 @@ def op_work(op):
         return "box_scores", 0.0, 4.0 * i[1] * i[2] * (i[0] + 5 * i[3])
     if k == O.BOX_CLASS_NMS:
         return "class_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 5
+    if k == O.GN_STATS:
+        return "group_norm", 0.0, 4.0 * i[0] * i[1] * i[2]
+    if k == O.RETINA_SELECT:
+        n = sum(i[11 + l] for l in range(i[1]))
+        return "retina_select", 0.0, 4.0 * i[0] * n * (i[3] + 4)
+    if k == O.RETINA_CLASS_NMS:
+        return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
     if k in (O.FORK, O.JOIN):
         return "lanes", 0.0, 0.0
     return f"kind{k}", 0.0, 0.0
@@ -272,7 +279,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="both", choices=["ssd", "frcnn", "both"])
+    ap.add_argument("--model", default="both", choices=["ssd", "frcnn", "retinanet", "both", "all"])
+    ap.add_argument("--retina-batch", type=int, default=8)
     ap.add_argument("--ssd-batch", type=int, default=32)
     ap.add_argument("--frcnn-batch", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
@@ -286,7 +294,7 @@ def main():
     from edgeml_amd import plan as plan_mod
     stream = torch.cuda.Stream()
     out = {}
-    if args.model in ("ssd", "both"):
+    if args.model in ("ssd", "both", "all"):
         B = args.ssd_batch
         m = models.ssdlite320_mobilenet_v3_large().to("cuda")
         plan = m.plan(B, 640, 640)
@@ -300,7 +308,20 @@ def main():
             attach_traffic(out["ssd"]["roofline"], "ssd")
         del plan
         m.plans.clear()
-    if args.model in ("frcnn", "both"):
+    if args.model in ("retinanet", "all"):
+        B = args.retina_batch
+        m = models.retinanet_resnet50_fpn_v2().to("cuda")
+        plan = m.plan(B, 640, 640)
+        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 70).cuda())
+        plan.capture(stream)
+        steps = max(1, args.steps // 2)
+        el = timed_steps(plan, stream, steps, max(1, args.warmup // 2), dist)
+        out["retinanet"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
+                            "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
+        if rank == 0 and not args.no_roofline:
+            out["retinanet"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "retinanet")
+        del plan
+    if args.model in ("frcnn", "both", "all"):
         B = args.frcnn_batch
         m = models.fasterrcnn_resnet50_fpn_v2().to("cuda")
         plan = m.plan(B, 640, 640)
@@ -324,15 +345,16 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    primary = "ssd" if "ssd" in out else "frcnn"
+    primary = "ssd" if "ssd" in out else ("frcnn" if "frcnn" in out else "retinanet")
     p = out[primary]
     line = {
         "metric": "images/sec/GPU at 640x640 (SSDLite & FRCNN-R50); ORIE max-abs-diff vs ref",
         "value": round(p["value"], 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(p["ms_per_step"], 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "ssdlite320_mobilenet_v3_large b=%d 640x640 (configs[1])" % p["batch"]
-                   if primary == "ssd" else "fasterrcnn_resnet50_fpn_v2 b=%d 640x640 (configs[2])" % p["batch"],
+        "config": {"workload": {"ssd": "ssdlite320_mobilenet_v3_large b=%d 640x640 (configs[1])",
+                                "frcnn": "fasterrcnn_resnet50_fpn_v2 b=%d 640x640 (configs[2])",
+                                "retinanet": "retinanet_resnet50_fpn_v2 b=%d 640x640"}[primary] % p["batch"],
                    "global_batch": p["batch"] * world, "parallelism": f"dp{world}",
                    "conv_math": plan_mod.CONV_MATH,
                    "weights": "seeded synthetic (COCO weights need a download)"},
@@ -342,6 +364,9 @@ def main():
         line["frcnn"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items() if k != "roofline"}
         if "roofline" in f:
             line["frcnn"]["roofline"] = f["roofline"]
+    if "retinanet" in out and primary != "retinanet":
+        f = out["retinanet"]
+        line["retinanet"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items()}
     if "roofline" in p:
         line["roofline"] = p["roofline"]
     line["dets_per_img"] = p.get("dets_per_img")

@@ -42,11 +42,13 @@ def ssd_default_boxes(grid_sizes, image_size=(320, 320), aspect_ratios=((2, 3),)
 
 
 def rpn_cell_anchors(size, ratios=(0.5, 1.0, 2.0)):
+    """AnchorGenerator.generate_anchors: one scale, or a tuple of scales (ratio-major order)."""
+    scales = np.asarray(size if isinstance(size, (tuple, list)) else [size], dtype=f32)
     ar = np.asarray(ratios, dtype=f32)
     hr = np.sqrt(ar).astype(f32)
     wr = (f32(1) / hr).astype(f32)
-    ws = (wr * f32(size)).astype(f32)
-    hs = (hr * f32(size)).astype(f32)
+    ws = (wr[:, None] * scales[None, :]).reshape(-1).astype(f32)
+    hs = (hr[:, None] * scales[None, :]).reshape(-1).astype(f32)
     base = np.stack([-ws, -hs, ws, hs], 1) / f32(2)
     return np.round(base).astype(f32)  # round-half-even, as torch.round
 
@@ -64,3 +66,12 @@ def rpn_anchors(grid_sizes, image_size, sizes=(32, 64, 128, 256, 512)):
         shifts = np.stack([xx, yy, xx, yy], 1).astype(f32)
         out.append((shifts[:, None, :] + base[None, :, :]).reshape(-1, 4).astype(f32))
     return out
+
+
+# retinanet _default_anchorgen(): sizes (x, int(x * 2^(1/3)), int(x * 2^(2/3))) per level, 3 ratios
+RETINA_SIZES = tuple((x, int(x * 2 ** (1.0 / 3)), int(x * 2 ** (2.0 / 3))) for x in (32, 64, 128, 256, 512))
+
+
+def retina_anchors(grid_sizes, image_size):
+    """Per level [gh*gw*9, 4] anchors of retinanet_resnet50_fpn_v2 (P3..P7), order (y, x, a)."""
+    return rpn_anchors(grid_sizes, image_size, sizes=RETINA_SIZES)

@@ -168,6 +168,50 @@ def frcnn_table(num_classes=91):
     return T.t
 
 
+RETINA_ANCHORS = 9  # 3 sizes x 3 aspect ratios per location (_default_anchorgen)
+
+
+def resnet50_body(T, p="backbone.body."):
+    """ResNet-50 v1.5 without avgpool/fc (IntermediateLayerGetter), BatchNorm2d."""
+    T.conv(p + "conv1", 64, 3, 7)
+    T.bn(p + "bn1", 64)
+    inplanes = 64
+    for name, nblk, width, stride in RESNET_LAYERS:
+        for b in range(nblk):
+            q = f"{p}{name}.{b}."
+            T.conv(q + "conv1", width, inplanes, 1)
+            T.bn(q + "bn1", width)
+            T.conv(q + "conv2", width, width, 3)
+            T.bn(q + "bn2", width)
+            T.conv(q + "conv3", width * 4, width, 1)
+            T.bn(q + "bn3", width * 4)
+            if b == 0:
+                T.conv(q + "downsample.0", width * 4, inplanes, 1)
+                T.bn(q + "downsample.1", width * 4)
+            inplanes = width * 4
+
+
+def retinanet_table(num_classes=91):
+    """state_dict (name -> shape) of retinanet_resnet50_fpn_v2 (detect.py:34-38): ResNet-50 body,
+    FPN over C3..C5 without norm (convs with bias) + LastLevelP6P7(2048, 256) (P6 from C5),
+    RetinaNetHead with GroupNorm(32) towers (4 x conv3x3 no bias + GN + ReLU) per branch."""
+    T = _Table()
+    resnet50_body(T)
+    for i, c in enumerate((512, 1024, 2048)):
+        T.conv(f"backbone.fpn.inner_blocks.{i}.0", 256, c, 1, bias=True)
+        T.conv(f"backbone.fpn.layer_blocks.{i}.0", 256, 256, 3, bias=True)
+    T.conv("backbone.fpn.extra_blocks.p6", 256, 2048, 3, bias=True)
+    T.conv("backbone.fpn.extra_blocks.p7", 256, 256, 3, bias=True)
+    for br, out, last in (("classification_head", RETINA_ANCHORS * num_classes, "cls_logits"),
+                          ("regression_head", RETINA_ANCHORS * 4, "bbox_reg")):
+        for i in range(4):
+            T.conv(f"head.{br}.conv.{i}.0", 256, 256, 3)
+            T.t[f"head.{br}.conv.{i}.1.weight"] = (256,)  # GroupNorm(32, 256)
+            T.t[f"head.{br}.conv.{i}.1.bias"] = (256,)
+        T.conv(f"head.{br}.{last}", out, 256, 3, bias=True)
+    return T.t
+
+
 def param_count(table):
     """Learnable parameters (what torchvision's model cards count): excludes BN buffers."""
     n = 0

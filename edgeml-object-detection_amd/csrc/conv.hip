@@ -47,6 +47,21 @@ __device__ __forceinline__ int64_t conv_row_offset(const ConvParams& p, int m, b
     return (int64_t)b * p.res_bstride + (int64_t)rpix * p.res_pstride;
 }
 
+// Input transform applied to in-bounds A-operand values (zero padding stays zero, as the reference
+// pads the transformed tensor): SqueezeExcitation's channel scale, GroupNorm's x * scale + shift
+// (ATen's GroupNorm forward form), and an optional ReLU.
+__device__ __forceinline__ f32x4 in_transform(const ConvParams& p, f32x4 v, int b, int ci) {
+    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)b * p.Cin + ci);
+    if (p.in_shift) v += *reinterpret_cast<const f32x4*>(p.in_shift + (int64_t)b * p.Cin + ci);
+    if (p.in_relu) {
+        v.x = v.x > 0.f ? v.x : 0.f;
+        v.y = v.y > 0.f ? v.y : 0.f;
+        v.z = v.z > 0.f ? v.z : 0.f;
+        v.w = v.w > 0.f ? v.w : 0.f;
+    }
+    return v;
+}
+
 template <int TM, int TN, int ACT>
 __device__ __forceinline__ void act_tile(floatx16 (&acc)[TM][TN]) {
 #pragma unroll
@@ -155,7 +170,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
         const int m = m0 + row;
         if (m < p.M && p.lin_x) {
             // 1x1 / stride 1 / pad 0 over a dense NHWC tensor: pixel m sits at m * pstride
-            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_b[j] = (p.in_scale || p.in_shift) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * p.x_pstride;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
@@ -192,13 +207,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
             f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
                 v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                if (p.in_scale) {
-                    const f32x4 s = *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
-                    v.x *= s.x;
-                    v.y *= s.y;
-                    v.z *= s.z;
-                    v.w *= s.w;
-                }
+                v = in_transform(p, v, a_b[j], ci);
             }
             ra[j] = v;
         }
@@ -311,7 +320,7 @@ __device__ __forceinline__ void pw_load(const ConvParams& p, PwFrag<TM, TN>& f, 
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if (aval[i] && k < p.K) {
                 v = *reinterpret_cast<const f32x4*>(arow[i] + k);
-                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)ab[i] * p.Cin + k);
+                v = in_transform(p, v, ab[i], k);
             }
             f.a[i][q] = v;
         }
@@ -342,7 +351,7 @@ __device__ __forceinline__ void pw_rows(const ConvParams& p, int m0, int n0, int
         const int m = m0 + i * 32 + l32;
         aval[i] = m < p.M;
         arow[i] = p.x + (int64_t)(aval[i] ? m : 0) * p.x_pstride;
-        ab[i] = (p.in_scale && aval[i]) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+        ab[i] = ((p.in_scale || p.in_shift) && aval[i]) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -512,7 +521,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
         const int row = (tid >> 2) + (NT / 4) * j;
         const int m = m0 + row;
         if (m < p.M && p.lin_x) {
-            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_b[j] = (p.in_scale || p.in_shift) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * p.x_pstride;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
@@ -573,7 +582,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (kval && (unsigned)(a_ih0[j] + kh) < (unsigned)p.H && (unsigned)(a_iw0[j] + kw) < (unsigned)p.W) {
                     v = *reinterpret_cast<const f32x4*>(a_row[j] + off);
-                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                    v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
             }
@@ -590,7 +599,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
                     v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                    if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                    v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
             }
@@ -739,7 +748,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     for (int j = 0; j < AJ; ++j) {
         const int m = m0 + (tid >> 3) + (NT / 8) * j;
         if (m < p.M && p.lin_x) {
-            a_b[j] = p.in_scale ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_b[j] = (p.in_scale || p.in_shift) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * p.x_pstride;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
@@ -781,7 +790,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
                 v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                if (p.in_scale) v *= *reinterpret_cast<const f32x4*>(p.in_scale + (int64_t)a_b[j] * p.Cin + ci);
+                v = in_transform(p, v, a_b[j], ci);
             }
             ra[j] = v;
         }

@@ -976,6 +976,162 @@ __global__ void __launch_bounds__(NT) box_class_nms_kernel(const float* __restri
     });
 }
 
+// ================================================================ RetinaNet postprocess
+// RetinaNet.postprocess_detections (retinanet_resnet50_fpn_v2, detect.py:34-38; oracle/retinanet.py):
+// per level: sigmoid over the flattened (anchor, class) logits, score > 0.05, topk(min(1000, n))
+// (score desc, flat index asc), decode (1,1,1,1) + clip -> candidate lists [B][L][topk];
+// then batched_nms(0.5) by label over the concatenated level lists and [:300].
+//
+// Two stages, so that a level of ~8M (anchor, class) scores is not one workgroup's work:
+// retina_chunk_select_kernel: one workgroup per (chunk of CH flat indices, level, image) keeps the
+//     chunk's top-k (score desc, index asc) unsorted in index order; every element of the level's
+//     top-k is in its chunk's top-k, so the union of the chunk lists (chunks in order) holds it with
+//     index order preserved;
+// retina_select_kernel: one workgroup per (level, image) selects the top-k of that union, sorts it,
+//     decodes and clips the boxes.
+template <int NT, int KC>
+__global__ void __launch_bounds__(NT) retina_chunk_select_kernel(RetinaSelParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
+    const int c = blockIdx.x, l = blockIdx.y, b = blockIdx.z;
+    const int K = P.K;
+    const int n = P.na[l] * K;
+    const int64_t slot = ((int64_t)(b * P.L + l) * P.nchunk + c);
+    const int start = c * P.chunk;
+    if (start >= n) {
+        if (threadIdx.x == 0) P.ccount[slot] = 0;
+        return;
+    }
+    const int nc = min(P.chunk, n - start);
+    const float* lg = P.logits + ((int64_t)b * P.Atot + P.a0[l]) * K + start;
+    const float thr = P.score_thresh;
+    auto fkey = [&](int i, uint32_t& k) -> bool {
+        const float s = 1.f / (1.f + expf(-lg[i]));
+        k = __float_as_uint(s);
+        return s > thr;
+    };
+    const uint32_t T = radix_select<NT>(nc, P.topk, fkey, S.hist, S.misc);
+    const bool take_all = S.misc[1] <= P.topk;
+    const int m = compact<NT>(nc, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    for (int t = threadIdx.x; t < m; t += NT) {
+        P.ckey[slot * KC + t] = (uint32_t)(S.keys[t] >> 32);
+        P.cidx[slot * KC + t] = start + key_index(S.keys[t]);
+    }
+    if (threadIdx.x == 0) P.ccount[slot] = m;
+}
+
+template <int NT, int KC>
+__global__ void __launch_bounds__(NT) retina_select_kernel(RetinaSelParams P, SegOut out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
+    const int l = blockIdx.x, b = blockIdx.y;
+    const int K = P.K;
+    const int n = P.na[l] * K;
+    const int nch = (n + P.chunk - 1) / P.chunk;
+    const int64_t base = (int64_t)(b * P.L + l) * P.nchunk;
+    const uint32_t* ck = P.ckey + base * KC;
+    const int* cc = P.ccount + base;
+    auto fkey = [&](int i, uint32_t& k) -> bool {  // i = chunk * KC + rank (index order preserved)
+        const int ch = i / KC, r = i - ch * KC;
+        k = ck[i];
+        return r < cc[ch];
+    };
+    const int n2 = nch * KC;
+    const uint32_t T = radix_select<NT>(n2, P.topk, fkey, S.hist, S.misc);
+    const bool take_all = S.misc[1] <= P.topk;
+    const int m = compact<NT>(n2, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    bitonic_desc<NT>(S.keys, nullptr, m);
+    const int seg = b * P.L + l;
+    for (int t = threadIdx.x; t < m; t += NT) {
+        const int i = P.cidx[base * KC + key_index(S.keys[t])];
+        const int a = P.a0[l] + i / K;
+        const f32x4 d = *reinterpret_cast<const f32x4*>(P.deltas + ((int64_t)b * P.Atot + a) * 4);
+        const f32x4 an = *reinterpret_cast<const f32x4*>(P.anchors + (int64_t)a * 4);
+        const int64_t o = (int64_t)seg * out.kmax + t;
+        out.box[o] = clip_box(decode_box(d, an, 1.f, 1.f, 1.f, 1.f), P.img_h, P.img_w);
+        out.score[o] = __uint_as_float((uint32_t)(S.keys[t] >> 32));
+        out.label[o] = i % K;
+        out.tb[o] = (uint32_t)(l * out.kmax + t);
+    }
+    if (threadIdx.x == 0) out.count[seg] = m;
+}
+
+// retina_class_nms_kernel: one workgroup per (class, image).  The class's candidates, in the
+// concatenated (level, rank) order, are taken KC at a time in (score desc, position asc) order (radix
+// select + ordered compaction, the next chunk strictly after the last key of the previous one);
+// each chunk is first suppressed by every box kept so far, then resolved greedily (nms_block).
+// Stops once out.kmax boxes are kept: later ones cannot enter the image's top out.kmax.
+template <int NT, int KC, int KEEP>
+__global__ void __launch_bounds__(NT) retina_class_nms_kernel(RetinaNmsParams P, SegOut out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
+    __shared__ f32x4 kept_box[KEEP];
+    __shared__ float kept_area[KEEP];
+    const int c = blockIdx.x, b = blockIdx.y;
+    const int n = P.L * P.kin;
+    const int64_t base = (int64_t)b * P.L * P.kin;
+    const int* cnt = P.count + b * P.L;
+    const int seg = b * P.K + c;
+    const int cap = out.kmax < KEEP ? out.kmax : KEEP;
+    uint32_t Tp = 0xffffffffu;
+    int Ip = -1;
+    bool first = true;
+    int kept = 0;
+    for (;;) {
+        auto fkey = [&](int i, uint32_t& k) -> bool {
+            const int l = i / P.kin, r = i - l * P.kin;
+            const float sc = P.score[base + i];
+            const int lb = P.label[base + i];
+            k = __float_as_uint(sc);
+            const bool after = first || k < Tp || (k == Tp && i > Ip);
+            return (r < cnt[l]) & (lb == c) & after;
+        };
+        const uint32_t T = radix_select<NT>(n, KC, fkey, S.hist, S.misc);
+        const bool take_all = S.misc[1] <= KC;
+        const int m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+        if (m == 0) break;
+        bitonic_desc<NT>(S.keys, nullptr, m);
+        for (int t = threadIdx.x; t < m; t += NT) {
+            const f32x4 bx = P.box[base + key_index(S.keys[t])];
+            const float ab = (bx.z - bx.x) * (bx.w - bx.y);
+            bool alive = true;
+            for (int q = 0; q < kept && alive; ++q)
+                if (iou_gt(kept_box[q], kept_area[q], bx, ab, P.iou)) alive = false;
+            S.box[t] = bx;
+            S.valid[t] = alive ? 1 : 0;
+        }
+        __syncthreads();
+        nms_block<NT, KC>(S, m, P.iou, false);
+        int written = 0;
+        for (int b0 = 0; b0 < m; b0 += NT) {
+            const int t = b0 + threadIdx.x;
+            const bool kf = t < m && S.valid[t];
+            int tot;
+            const int pos = BlockScan<NT>::exclusive(kf ? 1 : 0, S.wsum, tot);
+            const int slot = kept + written + pos;
+            if (kf && slot < cap) {
+                const int i = key_index(S.keys[t]);
+                const int64_t o = (int64_t)seg * out.kmax + slot;
+                out.box[o] = S.box[t];
+                out.score[o] = __uint_as_float((uint32_t)(S.keys[t] >> 32));
+                out.tb[o] = (uint32_t)i;  // concatenation order (level, rank)
+                out.label[o] = c;
+                kept_box[slot] = S.box[t];
+                kept_area[slot] = (S.box[t].z - S.box[t].x) * (S.box[t].w - S.box[t].y);
+            }
+            written += tot;
+        }
+        kept = kept + written < cap ? kept + written : cap;
+        const unsigned long long last = S.keys[m - 1];
+        __syncthreads();
+        if (take_all || kept >= cap) break;
+        Tp = (uint32_t)(last >> 32);
+        Ip = key_index(last);
+        first = false;
+    }
+    if (threadIdx.x == 0) out.count[seg] = kept;
+}
+
 // ================================================================ unit (batched) NMS for the C API
 template <int NT, int KC>
 __global__ void __launch_bounds__(NT) unit_nms_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
@@ -1215,6 +1371,41 @@ int box_class_nms_launch(const float* scores, const float* boxes, const int* cou
     if (set_lds(k, seg_smem<KC>())) return -2;
     hipLaunchKernelGGL(k, dim3(NC - 1, B), dim3(NT), seg_smem<KC>(), s, scores, (const f32x4*)boxes, counts, R, NC,
                        score_thresh, min_size, make_iou_thr(iou), out);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+int retina_select_launch(const RetinaSelParams& P, SegOut out, hipStream_t s) {
+    EDGEDET_REQUIRE(P.logits && P.deltas && P.anchors && seg_ok(out), "retina_select: null pointer");
+    EDGEDET_REQUIRE(P.L >= 1 && P.L <= 5 && P.topk > 0 && P.topk <= 1024 && out.kmax >= P.topk,
+                    "retina_select: 1..5 levels, topk <= 1024 <= kmax");
+    for (int l = 0; l < P.L; ++l)
+        EDGEDET_REQUIRE(P.na[l] > 0 && (int64_t)P.na[l] * P.K < (1ll << 31) && P.a0[l] + P.na[l] <= P.Atot,
+                        "retina_select: bad level extent");
+    EDGEDET_REQUIRE(P.ckey && P.cidx && P.ccount && P.chunk > 0 && P.nchunk > 0, "retina_select: null scratch");
+    for (int l = 0; l < P.L; ++l)
+        EDGEDET_REQUIRE(((int64_t)P.na[l] * P.K + P.chunk - 1) / P.chunk <= P.nchunk, "retina_select: scratch too small");
+    constexpr int KC = 1024, NT = 512;
+    auto k1 = retina_chunk_select_kernel<NT, KC>;
+    if (set_lds(k1, seg_smem<KC>())) return -2;
+    hipLaunchKernelGGL(k1, dim3(P.nchunk, P.L, P.B), dim3(NT), seg_smem<KC>(), s, P);
+    EDGEDET_LAUNCH_CHECK();
+    auto k2 = retina_select_kernel<NT, KC>;
+    if (set_lds(k2, seg_smem<KC>())) return -2;
+    hipLaunchKernelGGL(k2, dim3(P.L, P.B), dim3(NT), seg_smem<KC>(), s, P, out);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+int retina_class_nms_launch(const RetinaNmsParams& P, int B, SegOut out, hipStream_t s) {
+    EDGEDET_REQUIRE(P.box && P.score && P.label && P.count && seg_ok(out), "retina_class_nms: null pointer");
+    EDGEDET_REQUIRE(P.L >= 1 && P.kin > 0 && P.K > 0 && out.kmax > 0 && out.kmax <= 512,
+                    "retina_class_nms: bad sizes (kmax <= 512)");
+    constexpr int KC = 512, NT = 512, KEEP = 512;
+    auto k = retina_class_nms_kernel<NT, KC, KEEP>;
+    const size_t lds = seg_smem<KC>();
+    if (set_lds(k, lds + KEEP * 20)) return -2;
+    hipLaunchKernelGGL(k, dim3(P.K, B), dim3(NT), lds, s, P, out);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

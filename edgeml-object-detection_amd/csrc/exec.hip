@@ -9,6 +9,7 @@
 //   MEMSET         p0 ptr; i0 bytes
 //   PREPROCESS     p0 x[B,3,H,W]; p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
 //   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0; p6 w3 bf16 planes|0;
+//                  p7 in_shift|0; i24 in_relu;
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
@@ -35,6 +36,13 @@
 //                  f0 score_thresh; f1 min_size; d0 iou
 //   SSD_POSTPROCESS p0 scores_t; p1 boxes; p2 pool_key; p3 pool_ref; p4 ratio|0; p5 out_box; p6 out_score;
 //                  p7 out_label|0; p8 out_count; i0..4 B,A,NC,topk,N; f0 score_thresh; d0 iou
+//   GN_STATS       p0 x[B,HW,C]; p1 gamma; p2 beta; p3 scale[B,C]; p4 shift[B,C]; i0..3 B,HW,C,G; f0 eps
+//   RETINA_SELECT  p0 logits[B,Atot,K]; p1 deltas[B,Atot,4]; p2 anchors[Atot,4]; p3..7 records
+//                  (box,score,tb,label,count) [B,L,kmax]; i0..4 B,L,Atot,K,topk; i5 kmax; i6..10 a0 per level;
+//                  i11..15 anchors per level; f0,f1 img_h,img_w; f2 score_thresh; p8..10 chunk scratch
+//                  (keys, flat indices [B,L,nchunk,1024], counts [B,L,nchunk]); i16 chunk; i17 nchunk
+//   RETINA_CLASS_NMS p0..4 level records (box,score,tb,label,count); p5..9 class records [B,K,kmax];
+//                  i0..4 B,L,kin,K,kmax; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 #include <mutex>
 #include <string>
@@ -74,6 +82,8 @@ static ConvParams conv_params(const edgedet_op& o) {
     p.res = P<const float>(o, 4);
     p.in_scale = P<const float>(o, 5);
     p.w3 = P<const void>(o, 6);
+    p.in_shift = P<const float>(o, 7);
+    p.in_relu = (int)I[24];
     p.B = (int)I[0];
     p.H = (int)I[1];
     p.W = (int)I[2];
@@ -245,6 +255,57 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
         case EDGEDET_OP_BOX_CLASS_NMS:
             return box_class_nms_launch(P<const float>(o, 0), P<const float>(o, 1), P<const int>(o, 2), (int)I[0],
                                         (int)I[1], (int)I[2], o.f[0], o.f[1], o.d[0], seg_out(o, 3, (int)I[3]), s);
+        case EDGEDET_OP_GN_STATS: {
+            GnParams p{};
+            p.x = P<const float>(o, 0);
+            p.gamma = P<const float>(o, 1);
+            p.beta = P<const float>(o, 2);
+            p.scale = P<float>(o, 3);
+            p.shift = P<float>(o, 4);
+            p.B = (int)I[0];
+            p.HW = (int)I[1];
+            p.C = (int)I[2];
+            p.G = (int)I[3];
+            p.eps = o.f[0];
+            return gn_stats_launch(p, s);
+        }
+        case EDGEDET_OP_RETINA_SELECT: {
+            RetinaSelParams p{};
+            p.logits = P<const float>(o, 0);
+            p.deltas = P<const float>(o, 1);
+            p.anchors = P<const float>(o, 2);
+            p.B = (int)I[0];
+            p.L = (int)I[1];
+            p.Atot = (int)I[2];
+            p.K = (int)I[3];
+            p.topk = (int)I[4];
+            EDGEDET_REQUIRE(p.L >= 1 && p.L <= 5, "retina_select: 1..5 levels");
+            for (int l = 0; l < p.L; ++l) {
+                p.a0[l] = (int)I[6 + l];
+                p.na[l] = (int)I[11 + l];
+            }
+            p.img_h = o.f[0];
+            p.img_w = o.f[1];
+            p.score_thresh = o.f[2];
+            p.ckey = P<uint32_t>(o, 8);
+            p.cidx = P<int>(o, 9);
+            p.ccount = P<int>(o, 10);
+            p.chunk = (int)I[16];
+            p.nchunk = (int)I[17];
+            return retina_select_launch(p, seg_out(o, 3, (int)I[5]), s);
+        }
+        case EDGEDET_OP_RETINA_CLASS_NMS: {
+            RetinaNmsParams p{};
+            p.box = P<const f32x4>(o, 0);
+            p.score = P<const float>(o, 1);
+            p.label = P<const int>(o, 3);
+            p.count = P<const int>(o, 4);
+            p.L = (int)I[1];
+            p.kin = (int)I[2];
+            p.K = (int)I[3];
+            p.iou = make_iou_thr(o.d[0]);
+            return retina_class_nms_launch(p, (int)I[0], seg_out(o, 5, (int)I[4]), s);
+        }
         case EDGEDET_OP_SSD_POSTPROCESS: {
             SsdPostParams p{};
             p.scores_t = P<const float>(o, 0);

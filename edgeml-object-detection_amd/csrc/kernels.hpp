@@ -14,6 +14,8 @@ struct ConvParams {
     const float* res;
     const float* in_scale;  // [B][Cin] or null (SE excitation)
     const void* w3;         // bf16 split planes [3][Cout][Kpad] or null (bf16x6 tiles)
+    const float* in_shift;  // [B][Cin] or null: input transform x * in_scale + in_shift (GroupNorm apply)
+    int in_relu;            // ReLU on the transformed input (GroupNorm + ReLU, LastLevelP6P7's relu(P6))
     int B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, act;
     int K, Kpad, M;
     int x_pstride, y_pstride, res_pstride;
@@ -121,6 +123,41 @@ struct SsdPostParams {
     double iou;
 };
 
+struct GnParams {
+    const float* x;      // [B][HW][C] NHWC
+    const float* gamma;  // [C]
+    const float* beta;   // [C]
+    float* scale;        // [B][C]  GroupNorm(x) = x * scale + shift
+    float* shift;        // [B][C]
+    int B, HW, C, G;
+    float eps;
+};
+
+struct RetinaSelParams {
+    const float* logits;   // [B][Atot][K]
+    const float* deltas;   // [B][Atot][4]
+    const float* anchors;  // [Atot][4]
+    int a0[5], na[5];      // anchors of each level: [a0, a0 + na)
+    int L, B, Atot, K, topk;
+    float img_h, img_w, score_thresh;
+    uint32_t* ckey;        // [B][L][nchunk][1024] chunk top-k keys (scratch)
+    int* cidx;             // [B][L][nchunk][1024] their flat indices within the level
+    int* ccount;           // [B][L][nchunk]
+    int chunk, nchunk;     // flat indices per chunk; chunks per level (capacity)
+};
+
+struct RetinaNmsParams {
+    const f32x4* box;      // per-(image, level) candidate lists [B][L][kin]
+    const float* score;
+    const int* label;
+    const int* count;      // [B][L]
+    int L, kin, K;
+    IouThr iou;
+};
+
+int gn_stats_launch(const GnParams& p, hipStream_t s);
+int retina_select_launch(const RetinaSelParams& P, SegOut out, hipStream_t s);
+int retina_class_nms_launch(const RetinaNmsParams& P, int B, SegOut out, hipStream_t s);
 int conv_prepare(ConvParams& p);
 int conv_resolve_tile(const ConvParams& p, int tile);
 int conv_launch(ConvParams p, int tile, hipStream_t s);

@@ -595,6 +595,66 @@ int roi_align_launch(const RoiParams& p, hipStream_t s) {
     return 0;
 }
 
+// ================================================================ GroupNorm statistics
+// RetinaNetHead's GroupNorm(32, 256) (retinanet_resnet50_fpn_v2, detect.py:34-38): per (image,
+// group) mean / biased variance over HW x C/G values, in float64 (deterministic fixed-order
+// reduction), then ATen's forward form GN(x) = x * scale + shift with scale = rstd * gamma and
+// shift = -scale * mean + beta (float).  The consumer conv applies it (+ ReLU) as it loads its A
+// operand (conv.hip in_transform), so the normalized tensor never reaches HBM.
+__global__ void __launch_bounds__(256) gn_stats_kernel(GnParams p) {
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int cpg = p.C / p.G;
+    const float* xb = p.x + (int64_t)b * p.HW * p.C + g * cpg;
+    double s1 = 0.0, s2 = 0.0;
+    for (int px = threadIdx.x; px < p.HW; px += 256) {
+        const float* r = xb + (int64_t)px * p.C;
+        for (int c = 0; c < cpg; c += 4) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(r + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s1 += (double)v[e];
+                s2 += (double)v[e] * (double)v[e];
+            }
+        }
+    }
+    __shared__ double red[2][4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_down(s1, o, 64);
+        s2 += __shfl_down(s2, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = s1;
+        red[1][w] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x < cpg) {
+        const double n = (double)p.HW * cpg;
+        const double S1 = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        const double S2 = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        const double mean = S1 / n;
+        double var = S2 / n - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        const float meanf = (float)mean;
+        const float rstd = 1.f / sqrtf((float)var + p.eps);
+        const int c = g * cpg + threadIdx.x;
+        const float sc = rstd * p.gamma[c];
+        p.scale[(int64_t)b * p.C + c] = sc;
+        p.shift[(int64_t)b * p.C + c] = -sc * meanf + p.beta[c];
+    }
+}
+
+int gn_stats_launch(const GnParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.gamma && p.beta && p.scale && p.shift, "group_norm: null pointer");
+    EDGEDET_REQUIRE(p.G > 0 && p.C % p.G == 0 && (p.C / p.G) % 4 == 0 && p.C / p.G <= 256,
+                    "group_norm: channels per group must be a multiple of 4 (<= 256)");
+    EDGEDET_REQUIRE(p.B > 0 && p.HW > 0 && ((uintptr_t)p.x & 15) == 0, "group_norm: bad sizes/alignment");
+    hipLaunchKernelGGL(gn_stats_kernel, dim3(p.G, p.B), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
 }  // namespace edgedet
 
 using namespace edgedet;

@@ -22,8 +22,10 @@ from . import fmt, models
 
 
 def load_weak_models(model_name: str, model_path: str, num_class: int):
-    """detect.py:15-42.  ``model_path == ""`` asks the reference for downloaded COCO weights; offline
-    this build substitutes seeded synthetic weights of the same architecture (edgeml_amd.synthetic)."""
+    """detect.py:15-42.  ``model_path == ""`` asks the reference for downloaded COCO weights (a
+    91-class model whatever --dataset says); offline this build substitutes seeded synthetic weights
+    of the same architecture (edgeml_amd.synthetic).  Any other model name is RetinaNet
+    (detect.py:34-38)."""
     sd = None
     if model_path != "":
         ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
@@ -31,14 +33,16 @@ def load_weak_models(model_name: str, model_path: str, num_class: int):
             else ckpt
     if model_name == "ssd":
         if sd is None:
-            return models.ssdlite320_mobilenet_v3_large(weights="DEFAULT", num_classes=num_class)
+            return models.ssdlite320_mobilenet_v3_large(weights="DEFAULT")
         reduced = tuple(sd["backbone.features.1.3.0.weight"].shape)[1] == 80
         return models.SSDLite320(sd, num_class, reduced)
     if model_name == "faster_rcnn":
         if sd is None:
-            return models.fasterrcnn_resnet50_fpn_v2(weights="DEFAULT", num_classes=num_class)
+            return models.fasterrcnn_resnet50_fpn_v2(weights="DEFAULT")
         return models.FasterRCNNFPNv2(sd, num_class)
-    raise NotImplementedError("retinanet_resnet50_fpn_v2 (detect.py:34-38) is not built yet (SURVEY.md §8f row 3)")
+    if sd is None:
+        return models.retinanet_resnet50_fpn_v2(weights="DEFAULT")
+    return models.RetinaNetFPNv2(sd, num_class)
 
 
 def read_image(path):
@@ -123,7 +127,7 @@ def getargs(argv=None):
     args.add_argument('save_dir', help="Directory to save the detection outputs.")
     args.add_argument('--dataset', type=str, default="coco", help="The dataset to process ('coco' or 'voc').")
     args.add_argument('--model', type=str, default="ssd",
-                      help="The object detector. Available choices include 'ssd' and 'faster_rcnn'.")
+                      help="The object detector: 'ssd', 'faster_rcnn', anything else = RetinaNet.")
     args.add_argument("--model-path", type=str, default="",
                       help="Location of the saved object detection model weights (torchvision state_dict keys).")
     args.add_argument("--batch", type=int, default=0, help="Images per engine call (0 = model default).")

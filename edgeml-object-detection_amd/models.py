@@ -107,6 +107,15 @@ class _Detector:
     def _is_dw(self, wkey):
         return False
 
+    def _conv_nobias(self, wkey):
+        """A conv without bias and without BatchNorm (RetinaNet GroupNorm towers): zero bias."""
+        key = ("cn", wkey)
+        if key not in self._w:
+            w = _np(self.sd[wkey]).astype(np.float32)
+            wp, K, Kpad, cin = pack_conv_weight(w)
+            self._w[key] = (self._conv_w(wp), self.pack.add(np.zeros(w.shape[0], np.float32)), K, Kpad, cin)
+        return self._w[key]
+
     def _conv_w(self, wp):
         """Pack a [Cout][Kpad] conv weight plus its three bf16 planes (the bf16x6 tiles' operand)."""
         ref = self.pack.add(wp)
@@ -380,9 +389,9 @@ class FasterRCNNFPNv2(_Detector):
         scale = min(float(self.MIN_SIZE) / min(H, W), float(self.MAX_SIZE) / max(H, W))
         return int(math.floor(H * scale)), int(math.floor(W * scale))
 
-    def build_plan(self, B, H, W, pack_only=False):
-        P = Plan(self.pack, self.device or "cpu")
-        NC = self.num_classes
+    def _lower_body(self, P, B, H, W):
+        """GeneralizedRCNNTransform + ResNet-50 body (shared with RetinaNet): returns the input buffer,
+        the sizes, the conv / maxpool emitters and C2..C5."""
         Ho, Wo = self.resized_size(H, W)
         Hp = (Ho + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
         Wp = (Wo + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
@@ -394,10 +403,12 @@ class FasterRCNNFPNv2(_Detector):
         cur = (x, (B, Hp, Wp, 4))
 
         def conv(cur, wkey, bnp, k, stride, act, res=None, res_hw=None, cin_pad=None, bias_key=None, name=None,
-                 tile=0):
+                 tile=0, in_scale=None, in_shift=None, in_relu=False, out=None):
             xb, xs = cur
             if bias_key is not None:
                 w, b, K, Kpad, cin = self._conv_bias(wkey, bias_key)
+            elif bnp is None:
+                w, b, K, Kpad, cin = self._conv_nobias(wkey)
             else:
                 w, b, K, Kpad, cin = self._conv_bn(wkey, bnp, self.BN_EPS, cin_pad)
             cout = int(self.sd[wkey].shape[0])
@@ -405,9 +416,15 @@ class FasterRCNNFPNv2(_Detector):
             Ho_ = (xs[1] + 2 * pad - k) // stride + 1
             Wo_ = (xs[2] + 2 * pad - k) // stride + 1
             ys = (xs[0], Ho_, Wo_, cout)
+            if out is not None:  # strided store into a concatenated buffer: (buf, pixel stride, batch stride, off)
+                y, yp, yb, yo = out
+                conv_op(P, xb, xs, w, b, cout, k, stride, pad, act, y, ys, K, Kpad, res=res, res_hw=res_hw,
+                        name=name or wkey, tile=tile, in_scale=in_scale, in_shift=in_shift, in_relu=in_relu,
+                        y_pstride=yp, y_bstride=yb, y_off=yo)
+                return (y, ys)
             y = P.buf(ys, name=name or wkey)
             conv_op(P, xb, xs, w, b, cout, k, stride, pad, act, y, ys, K, Kpad, res=res, res_hw=res_hw,
-                    name=name or wkey, tile=tile)
+                    name=name or wkey, tile=tile, in_scale=in_scale, in_shift=in_shift, in_relu=in_relu)
             return (y, ys)
 
         def maxpool(cur, k, stride, pad, name):
@@ -437,6 +454,13 @@ class FasterRCNNFPNv2(_Detector):
                     idn = cur
                 cur = conv(y, q + "conv3.weight", q + "bn3", 1, 1, "RE", res=idn[0])
             cs.append(cur)
+
+        return inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs
+
+    def build_plan(self, B, H, W, pack_only=False):
+        P = Plan(self.pack, self.device or "cpu")
+        NC = self.num_classes
+        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W)
 
         # ---- FPN (BN, no activations) + LastLevelMaxPool
         f = "backbone.fpn."
@@ -559,6 +583,128 @@ class FasterRCNNFPNv2(_Detector):
         return P
 
 
+class RetinaNetFPNv2(FasterRCNNFPNv2):
+    """retinanet_resnet50_fpn_v2 (detect.py:34-38, the CLI's third model; oracle/retinanet.py).
+
+    Shares the transform and the ResNet-50 body with Faster R-CNN.  FPN over C3..C5 with plain convs
+    (bias, no norm) + LastLevelP6P7(2048, 256) (P6 on C5, P7 on relu(P6): the ReLU is applied as P7's
+    conv loads its input).  The GroupNorm towers of the head never materialise a normalised tensor:
+    GN_STATS turns each conv's output into per-(image, channel) scale / shift, which the next conv
+    applies (with the ReLU) as it loads its A operand.  The cls / box convs of every level store
+    straight into the concatenated [B, sum(HWA), K] / [B, sum(HWA), 4] tensors.
+    """
+
+    kind = "retinanet"
+    SCORE, NMS, DETS, TOPK = 0.05, 0.5, 300, 1000
+    GN_GROUPS, GN_EPS = 32, 1e-5
+    A = arch.RETINA_ANCHORS
+    SELECT_CHUNK = 1 << 16  # flat (anchor, class) indices per first-stage select workgroup
+
+    def table(self):
+        return arch.retinanet_table(self.num_classes)
+
+    def _gn(self, p):
+        key = ("gn", p)
+        if key not in self._w:
+            self._w[key] = (self.pack.add(_np(self.sd[p + ".weight"])), self.pack.add(_np(self.sd[p + ".bias"])))
+        return self._w[key]
+
+    def build_plan(self, B, H, W, pack_only=False):
+        P = Plan(self.pack, self.device or "cpu")
+        K, A = self.num_classes, self.A
+        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W)
+        f = "backbone.fpn."
+        c3, c4, c5 = cs[1], cs[2], cs[3]
+        last = conv(c5, f + "inner_blocks.2.0.weight", None, 1, 1, None, bias_key=f + "inner_blocks.2.0.bias")
+        outs = [conv(last, f + "layer_blocks.2.0.weight", None, 3, 1, None, bias_key=f + "layer_blocks.2.0.bias")]
+        for i, c in ((1, c4), (0, c3)):
+            last = conv(c, f"{f}inner_blocks.{i}.0.weight", None, 1, 1, None, bias_key=f"{f}inner_blocks.{i}.0.bias",
+                        res=last[0], res_hw=(last[1][1], last[1][2]))
+            outs.insert(0, conv(last, f"{f}layer_blocks.{i}.0.weight", None, 3, 1, None,
+                                bias_key=f"{f}layer_blocks.{i}.0.bias"))
+        p6 = conv(c5, f + "extra_blocks.p6.weight", None, 3, 2, None, bias_key=f + "extra_blocks.p6.bias")
+        p7 = conv(p6, f + "extra_blocks.p7.weight", None, 3, 2, None, bias_key=f + "extra_blocks.p7.bias",
+                  in_relu=True)
+        outs += [p6, p7]
+        branches = (("classification_head", "cls_logits", K), ("regression_head", "bbox_reg", 4))
+        if pack_only:
+            for br, last_name, _ in branches:
+                for i in range(4):
+                    self._conv_nobias(f"head.{br}.conv.{i}.0.weight")
+                    self._gn(f"head.{br}.conv.{i}.1")
+                self._conv_bias(f"head.{br}.{last_name}.weight", f"head.{br}.{last_name}.bias")
+            return P
+
+        grids = [(o[1][1], o[1][2]) for o in outs]
+        na = [gh * gw * A for gh, gw in grids]
+        a0 = [int(v) for v in np.concatenate([[0], np.cumsum(na)[:-1]])]
+        Atot = int(sum(na))
+        cls = P.buf((B, Atot, K), name="head.cls_logits")
+        reg = P.buf((B, Atot, 4), name="head.bbox_regression")
+        C = 256
+        P.fork(3)  # the five levels' head towers are independent
+        for lvl, fm in enumerate(outs):
+            P.lane(lvl % 4)
+            hw = fm[1][1] * fm[1][2]
+            for br, last_name, kk in branches:
+                dst = cls if kk == K else reg
+                t, sc, sh = fm, None, None
+                for i in range(4):
+                    q = f"head.{br}.conv.{i}."
+                    t = conv(t, q + "0.weight", None, 3, 1, None, in_scale=sc, in_shift=sh, in_relu=i > 0,
+                             name=f"{q}0@{lvl}")
+                    gamma, beta = self._gn(q + "1")
+                    sc = P.buf((B, C), name=f"{q}1.scale@{lvl}")
+                    sh = P.buf((B, C), name=f"{q}1.shift@{lvl}")
+                    P.add(Op(ops.GN_STATS, {0: B, 1: hw, 2: C, 3: self.GN_GROUPS},
+                             {0: t[0], 1: gamma, 2: beta, 3: sc, 4: sh}, {0: self.GN_EPS}, name=f"{q}1@{lvl}"))
+                conv(t, f"head.{br}.{last_name}.weight", None, 3, 1, None, bias_key=f"head.{br}.{last_name}.bias",
+                     in_scale=sc, in_shift=sh, in_relu=True, out=(dst, A * kk, Atot * kk, a0[lvl] * kk),
+                     name=f"head.{br}.{last_name}@{lvl}")
+        P.join()
+        anchors = P.const(np.concatenate(anc.retina_anchors(grids, (Hp, Wp)), 0), name="anchors")
+
+        # ---- RetinaNet.postprocess_detections
+        L, KM = len(outs), self.TOPK
+        lrec = [P.buf((B, L, KM, 4), name="retina.cand.box"), P.buf((B, L, KM), name="retina.cand.score"),
+                P.buf((B, L, KM), torch.int32, name="retina.cand.tb"),
+                P.buf((B, L, KM), torch.int32, name="retina.cand.label"),
+                P.buf((B, L), torch.int32, name="retina.cand.count")]
+        CH = self.SELECT_CHUNK
+        nchunk = max(-(-n * K // CH) for n in na)
+        ck = P.buf((B, L, nchunk, 1024), torch.int32, name="retina.chunk.key")
+        ci = P.buf((B, L, nchunk, 1024), torch.int32, name="retina.chunk.idx")
+        cc = P.buf((B, L, nchunk), torch.int32, name="retina.chunk.count")
+        si = {0: B, 1: L, 2: Atot, 3: K, 4: self.TOPK, 5: KM, 16: CH, 17: nchunk}
+        for l in range(L):
+            si[6 + l], si[11 + l] = a0[l], na[l]
+        P.add(Op(ops.RETINA_SELECT, si, {0: cls, 1: reg, 2: anchors, 3: lrec[0], 4: lrec[1], 5: lrec[2],
+                                         6: lrec[3], 7: lrec[4], 8: ck, 9: ci, 10: cc},
+                 {0: Ho, 1: Wo, 2: self.SCORE}, name="retina.select_topk"))
+        N = self.DETS
+        crec = [P.buf((B, K, N, 4), name="retina.kept.box"), P.buf((B, K, N), name="retina.kept.score"),
+                P.buf((B, K, N), torch.int32, name="retina.kept.tb"), P.buf((B, K, N), torch.int32, name="retina.kept.lbl"),
+                P.buf((B, K), torch.int32, name="retina.kept.count")]
+        P.add(Op(ops.RETINA_CLASS_NMS, {0: B, 1: L, 2: KM, 3: K, 4: N},
+                 {0: lrec[0], 1: lrec[1], 2: lrec[2], 3: lrec[3], 4: lrec[4], 5: crec[0], 6: crec[1], 7: crec[2],
+                  8: crec[3], 9: crec[4]}, d={0: self.NMS}, name="retina.batched_nms"))
+        ratio = np.tile(np.asarray([np.float32(W) / np.float32(Wo), np.float32(H) / np.float32(Ho)], np.float32),
+                        (B, 1))
+        ratio_b = P.const(ratio, name="ratio")
+        P.out_box = P.buf((B, N, 4), name="out.boxes")
+        P.out_score = P.buf((B, N), name="out.scores")
+        P.out_label = P.buf((B, N), torch.int64, name="out.labels")
+        P.out_count = P.buf((B,), torch.int32, name="out.count")
+        P.add(Op(ops.MERGE_TOPK, {0: B, 1: K, 2: N, 3: N},
+                 {0: crec[0], 1: crec[1], 2: crec[2], 3: crec[3], 4: crec[4], 5: ratio_b, 6: P.out_box,
+                  7: P.out_score, 8: P.out_label, 9: P.out_count}, name="retina.detections_per_img"))
+        P.input = inp
+        P.feats = [o[0] for o in outs]
+        P.cls_logits, P.bbox_regression = cls, reg
+        P.cand_count = lrec[4]
+        return P
+
+
 # ====================================================================================== factories
 def ssdlite320_mobilenet_v3_large(weights=None, num_classes=91, reduced_tail=True, state_dict=None, seed=0):
     """Builder mirroring torchvision's (detect.py:24,26).  ``weights="DEFAULT"`` would download COCO
@@ -576,3 +722,11 @@ def fasterrcnn_resnet50_fpn_v2(weights=None, num_classes=91, state_dict=None, se
     if state_dict is None:
         state_dict = synthetic.synthetic_state_dict("faster_rcnn", num_classes, seed=seed)
     return FasterRCNNFPNv2(state_dict, num_classes)
+
+
+def retinanet_resnet50_fpn_v2(weights=None, num_classes=91, state_dict=None, seed=0):
+    """Builder mirroring torchvision's (detect.py:36,38); see ssdlite320_mobilenet_v3_large."""
+    from . import synthetic
+    if state_dict is None:
+        state_dict = synthetic.synthetic_state_dict("retinanet", num_classes, seed=seed)
+    return RetinaNetFPNv2(state_dict, num_classes)

@@ -20,6 +20,7 @@ OP_INTS, OP_PTRS, OP_DBLS, OP_FLTS = 48, 24, 8, 16
 MEMSET, PREPROCESS, CONV, DWCONV, CHANNEL_MEAN, SE_FC, MAXPOOL = 1, 2, 3, 4, 5, 6, 7
 SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX_CLASS_NMS = 8, 9, 10, 11, 12, 13, 14
 FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
+GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)

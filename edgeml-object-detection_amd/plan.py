@@ -278,7 +278,7 @@ class Plan:
 # ------------------------------------------------------------------------------ op helpers
 def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K, Kpad, res=None, res_hw=None,
             in_scale=None, y_pstride=None, y_bstride=None, y_off=0, x_pstride=None, x_bstride=None, tile=0,
-            name=""):
+            name="", in_shift=None, in_relu=False):
     """Build a CONV record.  x_shape = (B, H, W, C) as laid out in x; y_shape = (B, Ho, Wo, Cout)."""
     B, H, W, C = x_shape
     _, Ho, Wo, _ = y_shape
@@ -290,6 +290,7 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
     i = {0: B, 1: H, 2: W, 3: C, 4: Ho, 5: Wo, 6: cout, 7: k, 8: k, 9: stride, 10: pad, 11: ops.ACT[act], 12: K,
          13: Kpad, 14: xp, 15: yp, 16: cout, 17: (H * W * xp if x_bstride is None else x_bstride),
          18: (Ho * Wo * yp if y_bstride is None else y_bstride), 19: rH * rW * cout, 20: y_off, 21: rH, 22: rW,
-         23: tile}
+         23: tile, 24: 1 if in_relu else 0}
     w3 = getattr(w, "split", None) if CONV_MATH == "bf16x6" else None
-    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale, 6: w3}, name=name))
+    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale, 6: w3, 7: in_shift},
+                       name=name))

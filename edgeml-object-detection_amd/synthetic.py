@@ -23,6 +23,8 @@ _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 def _variant(kind, num_classes, reduced_tail):
     if kind == "ssd":
         return f"ssd_{'reduced' if reduced_tail else 'full'}_{num_classes}"
+    # RetinaNet's only BatchNorms are the ResNet-50 body's, drawn first from the same seeded stream as
+    # Faster R-CNN's body and fed the same transform: its calibration is FRCNN's body statistics.
     return f"frcnn_{num_classes}"
 
 
@@ -35,6 +37,8 @@ def table_for(kind, num_classes=91, reduced_tail=True):
         return arch.ssdlite_table(num_classes, reduced_tail)
     if kind == "faster_rcnn":
         return arch.frcnn_table(num_classes)
+    if kind == "retinanet":
+        return arch.retinanet_table(num_classes)
     raise ValueError(kind)
 
 
@@ -45,6 +49,11 @@ def _head_gain(kind, name):
             return 1.5, None
         if name.startswith("head.regression_head") and name.endswith(".1.weight"):
             return 0.7, None
+    elif kind == "retinanet":
+        if name == "head.classification_head.cls_logits.weight":
+            return 0.7, None  # logits ~ prior bias +- 0.7: a few thousand (anchor, class) scores > 0.05
+        if name == "head.regression_head.bbox_reg.weight":
+            return 0.15, None
     else:
         if name == "rpn.head.cls_logits.weight":
             return 1.5, None
@@ -59,7 +68,7 @@ def _head_gain(kind, name):
 
 def _is_residual_bn(kind, name):
     """Last BN of a residual branch (zero-init-residual style small gamma keeps random nets stable)."""
-    if kind == "faster_rcnn":
+    if kind in ("faster_rcnn", "retinanet"):
         return bool(re.search(r"layer\d\.\d+\.bn3\.weight$", name))
     return False
 
@@ -81,6 +90,10 @@ def synthetic_state_dict(kind, num_classes=91, reduced_tail=True, seed=0, calibr
             continue
         is_bn = name.endswith(".weight") and (name[:-len(".weight")] + ".running_mean") in table
         is_bn_bias = name.endswith(".bias") and (name[:-len(".bias")] + ".running_mean") in table
+        if len(shape) == 1 and name.endswith(".weight") and ".conv." in name and kind == "retinanet":
+            is_bn = True  # GroupNorm affine
+        if len(shape) == 1 and name.endswith(".bias") and ".conv." in name and kind == "retinanet":
+            is_bn_bias = True
         if is_bn:
             lo, hi = (0.2, 0.4) if _is_residual_bn(kind, name) else (0.8, 1.2)
             sd[name] = torch.empty(shape).uniform_(lo, hi, generator=g)
@@ -92,6 +105,8 @@ def synthetic_state_dict(kind, num_classes=91, reduced_tail=True, seed=0, calibr
                 b.view(6, num_classes)[:, 0] += 2.0     # background logit per anchor
             if kind == "faster_rcnn" and name == "roi_heads.box_predictor.cls_score.bias":
                 b[0] += 2.0
+            if kind == "retinanet" and name == "head.classification_head.cls_logits.bias":
+                b += -math.log((1 - 0.01) / 0.01)  # torchvision's prior-probability init
             sd[name] = b
         else:
             fan_in = 1
@@ -102,12 +117,15 @@ def synthetic_state_dict(kind, num_classes=91, reduced_tail=True, seed=0, calibr
             sd[name] = torch.randn(shape, generator=g) * std
     if calibrated:
         path = calib_path(kind, num_classes, reduced_tail)
+        if not os.path.exists(path):  # other class counts: the class-independent BN layers of the 91
+            path = calib_path(kind, 91, reduced_tail)
         if not os.path.exists(path):
             raise FileNotFoundError(f"BN calibration table missing: {path} "
                                     f"(regenerate with tests/golden/make_calibration.py)")
         with np.load(path, allow_pickle=False) as z:
             for k in z.files:
-                sd[k] = torch.from_numpy(z[k].astype(np.float32))
+                if k in table and tuple(z[k].shape) == tuple(table[k]):
+                    sd[k] = torch.from_numpy(z[k].astype(np.float32))
     return sd
 
 

@@ -63,7 +63,10 @@ enum {
     EDGEDET_OP_BOX_CLASS_NMS = 14,/* per (image, class): score>t, remove_small, NMS                   */
     EDGEDET_OP_FORK = 15,         /* side lanes 1..i[0] wait for everything issued so far on lane 0    */
     EDGEDET_OP_JOIN = 16,         /* lane 0 waits for everything issued so far on lanes 1..i[0]        */
-    EDGEDET_OP_SSD_POSTPROCESS = 17 /* per image: class top-k pool, global-order greedy NMS, [:N]      */
+    EDGEDET_OP_SSD_POSTPROCESS = 17,/* per image: class top-k pool, global-order greedy NMS, [:N]      */
+    EDGEDET_OP_GN_STATS = 18,     /* GroupNorm statistics -> per (image, channel) scale / shift       */
+    EDGEDET_OP_RETINA_SELECT = 19,/* RetinaNet per (image, level): sigmoid > t, top-k, decode, clip   */
+    EDGEDET_OP_RETINA_CLASS_NMS = 20 /* RetinaNet per (image, class): NMS over the level candidates  */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,

@@ -209,8 +209,9 @@ def ssd_default_boxes(grid_sizes, image_size=(320, 320), aspect_ratios=((2, 3),)
 
 
 def rpn_cell_anchors(size, ratios=(0.5, 1.0, 2.0)):
-    """AnchorGenerator.generate_anchors for one level."""
-    scales = torch.as_tensor([size], dtype=torch.float32)
+    """AnchorGenerator.generate_anchors for one level; size = one scale or a
+    tuple of scales (ratio-major, scale-minor order)."""
+    scales = torch.as_tensor(size if isinstance(size, (tuple, list)) else [size], dtype=torch.float32)
     ar = torch.as_tensor(ratios, dtype=torch.float32)
     hr = torch.sqrt(ar)
     wr = 1 / hr
@@ -231,6 +232,14 @@ def rpn_anchors(grid_sizes, image_size, sizes=(32, 64, 128, 256, 512)):
         shifts = torch.stack((xx, yy, xx, yy), dim=1)
         out.append((shifts.view(-1, 1, 4) + base.view(1, -1, 4)).reshape(-1, 4))
     return out
+
+
+RETINA_SIZES = tuple((x, int(x * 2 ** (1.0 / 3)), int(x * 2 ** (2.0 / 3))) for x in (32, 64, 128, 256, 512))
+
+
+def retina_anchors(grid_sizes, image_size):
+    """retinanet _default_anchorgen(): 3 sizes x 3 ratios per location, per level (P3..P7)."""
+    return rpn_anchors(grid_sizes, image_size, sizes=RETINA_SIZES)
 
 
 # ---------------------------------------------------------------- RoIAlign (SURVEY A.2 step 5)

@@ -16,6 +16,7 @@ def test_param_counts_match_published():
     assert arch.param_count(arch.ssdlite_table(91, True)) == 3_440_060
     assert arch.param_count(arch.ssdlite_table(91, False)) == 5_198_540
     assert arch.param_count(arch.frcnn_table(91)) == 43_712_278
+    assert arch.param_count(arch.retinanet_table(91)) == 38_198_935  # RetinaNet_ResNet50_FPN_V2_Weights
 
 
 def test_ssd_anchors_match_oracle():
@@ -218,3 +219,16 @@ def test_reward_entries_sorted_by_class_then_conf():
     np.testing.assert_array_equal(img, [0, 0, 1, 0, 1])       # conf .95(s), .9(w,img0), .9(s,img1), .2 | 3: .3
     np.testing.assert_array_equal(flag >> 1, [1, 0, 1, 0, 1])
     np.testing.assert_array_equal(lab_cnt, [[1, 1], [0, 0]])
+
+
+@pytest.mark.parametrize("hp,wp", [(800, 800), (608, 800)])
+def test_retina_anchors_match_oracle(hp, wp):
+    import numpy as np
+    from edgeml_amd import anchors
+    from oracle import tv_ops
+    grids = [((hp + s - 1) // s, (wp + s - 1) // s) for s in (8, 16, 32, 64, 128)]
+    ours = anchors.retina_anchors(grids, (hp, wp))
+    ref = tv_ops.retina_anchors(grids, (hp, wp))
+    for a, b in zip(ours, ref):
+        assert a.shape[0] == b.shape[0] and a.shape[0] % 9 == 0
+        np.testing.assert_array_equal(a, b.numpy())
