@@ -10,6 +10,7 @@ the forward into one op list per input shape; ops.py loads the library and fails
 missing).  Architecture and post-processing constants: SURVEY.md Appendix A.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -17,7 +18,7 @@ import torch
 from . import anchors as anc
 from . import arch
 from . import ops
-from .plan import Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight, split_bf16x3
+from .plan import BufView, Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight, split_bf16x3
 
 
 def _np(t):
@@ -175,6 +176,7 @@ class SSDLite320(_Detector):
     # "image": SSD_POSTPROCESS (class top-k pool + one global-order greedy pass per image);
     # "class": SSD_CLASS_NMS + MERGE_TOPK (every class's top-k fully NMS'd, then merged).
     postprocess = "image"
+    CHAINS = 2
     IMAGE_POOL_MAX = 512 * 54  # (classes - 1) * TOPK that fits the image kernel's registers
 
     def __init__(self, state_dict, num_classes=91, reduced_tail=None, device=None):
@@ -202,13 +204,47 @@ class SSDLite320(_Detector):
                             self.pack.add(w2.T), self.pack.add(_np(self.sd[p + ".fc2.bias"])), w1.shape[0])
         return self._w[key]
 
+    def n_chains(self, B):
+        """Independent sub-batches lowered as concurrent chains (stream lanes): SSDLite's layers are
+        small, so two chains overlap one chain's latency-bound tail (NMS) and small kernels with the
+        other's work.  EDGEDET_SSD_CHAINS overrides (1 = one chain)."""
+        n = int(os.environ.get("EDGEDET_SSD_CHAINS", "0")) or self.CHAINS
+        n = max(1, min(n, ops.MAX_LANES, B // 8 if B >= 16 else 1))
+        while B % n:
+            n -= 1
+        return n
+
     def build_plan(self, B, H, W, pack_only=False):
         P = Plan(self.pack, self.device or "cpu")
+        nch = 1 if pack_only else self.n_chains(B)
+        inp = P.buf((B, 3, H, W), name="images")
+        shared = {}
+        if nch > 1:
+            P.fork(nch - 1)
+        for c in range(nch):
+            if nch > 1:
+                P.lane(c)
+            self._lower_chain(P, c, B // nch, B, H, W, inp, shared, nch, pack_only)
+            if pack_only:
+                return P
+        if nch > 1:
+            P.join()
+        P.input = inp
+        P.cls_logits, P.bbox_regression = shared["cls"], shared["reg"]
+        P.scores_t, P.boxes = shared["scores_t"], shared["boxes"]
+        P.out_box, P.out_score, P.out_label, P.out_count = (shared[k] for k in ("ob", "os", "ol", "oc"))
+        P.feats = shared["feats"]
+        P.chains = nch
+        return P
+
+    def _lower_chain(self, P, c, B, Btot, H, W, inp, shared, nch, pack_only):
+        """Lower the forward of images [c*B, (c+1)*B) (B per chain, Btot in the plan)."""
         NC = self.num_classes
         S = self.SIZE
-        inp = P.buf((B, 3, H, W), name="images")
-        x = P.buf((B, S, S, 4), name="pre")
-        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {0: inp, 1: x},
+        sfx = f"#{c}" if nch > 1 else ""
+        view = (lambda buf: BufView(buf, c * B, B)) if nch > 1 else (lambda buf: buf)
+        x = P.buf((B, S, S, 4), name="pre" + sfx)
+        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {0: view(inp), 1: x},
                  {0: 0.5, 1: 0.5, 2: 0.5, 3: 0.5, 4: 0.5, 5: 0.5}, name="transform"))
         cur = (x, (B, S, S, 4))
 
@@ -219,7 +255,7 @@ class SSDLite320(_Detector):
             Ho = (xs[1] + 2 * ((k - 1) // 2) - k) // stride + 1
             Wo = (xs[2] + 2 * ((k - 1) // 2) - k) // stride + 1
             ys = (B, Ho, Wo, cout)
-            y = P.buf(ys, name=prefix)
+            y = P.buf(ys, name=prefix + sfx)
             conv_op(P, xb, xs, w, b, cout, k, stride, (k - 1) // 2, act, y, ys, K, Kpad, res=res,
                     in_scale=in_scale, name=prefix)
             return (y, ys)
@@ -232,9 +268,9 @@ class SSDLite320(_Detector):
             Ho = (xs[1] + 2 * pad - k) // stride + 1
             Wo = (xs[2] + 2 * pad - k) // stride + 1
             ys = (B, Ho, Wo, xs[3])
-            y = P.buf(ys, name=prefix)
+            y = P.buf(ys, name=prefix + sfx)
             parts = ops.se_parts(Ho, Wo)
-            part = P.buf((B, parts, xs[3]), name=prefix + ".se_partial_sums") if se_part else None
+            part = P.buf((B, parts, xs[3]), name=prefix + ".se_partial_sums" + sfx) if se_part else None
             P.add(Op(ops.DWCONV, {0: B, 1: xs[1], 2: xs[2], 3: xs[3], 4: Ho, 5: Wo, 6: k, 7: stride, 8: pad,
                                   9: ops.ACT[act], 10: parts}, {0: xb, 1: w, 2: b, 3: y, 4: part}, name=prefix))
             return (y, ys, (part, parts)) if se_part else (y, ys)
@@ -244,8 +280,8 @@ class SSDLite320(_Detector):
             xb, xs, (part, parts) = cur
             w1, b1, w2t, b2, sq = self._se(p)
             C = xs[3]
-            scale = P.buf((B, C), name=p + ".scale")
-            hidden = P.buf((B, sq), name=p + ".hidden")
+            scale = P.buf((B, C), name=p + ".scale" + sfx)
+            hidden = P.buf((B, sq), name=p + ".hidden" + sfx)
             P.add(Op(ops.SE_FC, {0: B, 1: C, 2: sq, 3: xs[1] * xs[2], 4: parts},
                      {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale, 6: hidden}, name=p))
             return scale
@@ -284,65 +320,72 @@ class SSDLite320(_Detector):
 
         grids = [(f[1][1], f[1][2]) for f in feats]
         A = sum(h * w * 6 for h, w in grids)
-        cls = P.buf((B, A, NC), name="cls_logits")
-        reg = P.buf((B, A, 4), name="bbox_regression")
+        if "cls" not in shared:
+            shared["cls"] = P.buf((Btot, A, NC), name="cls_logits")
+            shared["reg"] = P.buf((Btot, A, 4), name="bbox_regression")
+            shared["feats"] = [f[0] for f in feats]
+        cls, reg = shared["cls"], shared["reg"]
         off = 0
-        # the 12 head branches are independent: spread them over 4 stream lanes
-        P.fork(3)
+        # the 12 head branches are independent: spread them over 4 stream lanes (one chain only)
+        if nch == 1:
+            P.fork(3)
         chain = 0
         for i, f in enumerate(feats):
             fb, fs = f
             for name, cols, out in (("classification_head", NC, cls), ("regression_head", 4, reg)):
                 p = f"head.{name}.module_list.{i}"
-                P.lane(chain % 4)
+                if nch == 1:
+                    P.lane(chain % 4)
                 chain += 1
                 t = dw(f, p + ".0", 3, 1, "R6")
                 w, b, K, Kpad, cin = self._conv_bias(p + ".1.weight", p + ".1.bias")
                 cout = 6 * cols
                 conv_op(P, t[0], t[1], w, b, cout, 1, 1, 0, None, out, (B, fs[1], fs[2], cout), K, Kpad,
-                        y_pstride=cout, y_bstride=A * cols, y_off=off * cols, name=p + ".1")
+                        y_pstride=cout, y_bstride=A * cols, y_off=c * B * A * cols + off * cols, name=p + ".1" + sfx)
             off += fs[1] * fs[2] * 6
-        P.join()
+        if nch == 1:
+            P.join()
         self.grids = grids
         if pack_only:
-            return P
+            return
 
-        anchors = P.const(anc.ssd_default_boxes(grids, (S, S)), name="anchors")
-        scores_t = P.buf((B, NC, A), name="scores_t")
-        boxes = P.buf((B, A, 4), name="boxes")
-        P.add(Op(ops.SSD_SCORES, {0: B, 1: A, 2: NC}, {0: cls, 1: reg, 2: anchors, 3: scores_t, 4: boxes},
-                 {0: S, 1: S}, name="postprocess.scores"))
+        if "anchors" not in shared:
+            shared["anchors"] = P.const(anc.ssd_default_boxes(grids, (S, S)), name="anchors")
+            shared["scores_t"] = P.buf((Btot, NC, A), name="scores_t")
+            shared["boxes"] = P.buf((Btot, A, 4), name="boxes")
+            ratio = np.tile(np.asarray([np.float32(W) / np.float32(S), np.float32(H) / np.float32(S)], np.float32),
+                            (Btot, 1))
+            shared["ratio"] = P.const(ratio, name="ratio")
+            shared["ob"] = P.buf((Btot, self.DETS, 4), name="out.boxes")
+            shared["os"] = P.buf((Btot, self.DETS), name="out.scores")
+            shared["ol"] = P.buf((Btot, self.DETS), torch.int64, name="out.labels")
+            shared["oc"] = P.buf((Btot,), torch.int32, name="out.count")
+        anchors = shared["anchors"]
+        scores_t, boxes = view(shared["scores_t"]), view(shared["boxes"])
+        P.add(Op(ops.SSD_SCORES, {0: B, 1: A, 2: NC}, {0: view(cls), 1: view(reg), 2: anchors, 3: scores_t, 4: boxes},
+                 {0: S, 1: S}, name="postprocess.scores" + sfx))
         NS, KM = NC - 1, self.TOPK
-        ratio = np.tile(np.asarray([np.float32(W) / np.float32(S), np.float32(H) / np.float32(S)], np.float32),
-                        (B, 1))
-        ratio_b = P.const(ratio, name="ratio")
-        P.out_box = P.buf((B, self.DETS, 4), name="out.boxes")
-        P.out_score = P.buf((B, self.DETS), name="out.scores")
-        P.out_label = P.buf((B, self.DETS), torch.int64, name="out.labels")
-        P.out_count = P.buf((B,), torch.int32, name="out.count")
+        ratio_b = view(shared["ratio"])
+        out_box, out_score, out_label, out_count = (view(shared[k]) for k in ("ob", "os", "ol", "oc"))
         if self.postprocess == "image" and NS * KM <= self.IMAGE_POOL_MAX and self.DETS <= 1024:
             # class top-k pool + global-order greedy NMS, stopping at DETS kept (csrc/detect.hip)
-            pool_key = P.buf((B, NS, KM), torch.int32, name="pool.key")
-            pool_ref = P.buf((B, NS, KM), torch.int32, name="pool.ref")
+            pool_key = P.buf((B, NS, KM), torch.int32, name="pool.key" + sfx)
+            pool_ref = P.buf((B, NS, KM), torch.int32, name="pool.ref" + sfx)
             P.add(Op(ops.SSD_POSTPROCESS, {0: B, 1: A, 2: NC, 3: KM, 4: self.DETS},
-                     {0: scores_t, 1: boxes, 2: pool_key, 3: pool_ref, 4: ratio_b, 5: P.out_box, 6: P.out_score,
-                      7: P.out_label, 8: P.out_count}, {0: self.SCORE_THRESH}, {0: self.NMS_THRESH},
-                     name="postprocess.nms"))
+                     {0: scores_t, 1: boxes, 2: pool_key, 3: pool_ref, 4: ratio_b, 5: out_box, 6: out_score,
+                      7: out_label, 8: out_count}, {0: self.SCORE_THRESH}, {0: self.NMS_THRESH},
+                     name="postprocess.nms" + sfx))
         else:
-            rec = [P.buf((B, NS, KM, 4), name="rec.box"), P.buf((B, NS, KM), name="rec.score"),
-                   P.buf((B, NS, KM), torch.int32, name="rec.tb"), P.buf((B, NS, KM), torch.int32, name="rec.label"),
-                   P.buf((B, NS), torch.int32, name="rec.count")]
+            rec = [P.buf((B, NS, KM, 4), name="rec.box" + sfx), P.buf((B, NS, KM), name="rec.score" + sfx),
+                   P.buf((B, NS, KM), torch.int32, name="rec.tb" + sfx),
+                   P.buf((B, NS, KM), torch.int32, name="rec.label" + sfx),
+                   P.buf((B, NS), torch.int32, name="rec.count" + sfx)]
             P.add(Op(ops.SSD_CLASS_NMS, {0: B, 1: A, 2: NC, 3: self.TOPK, 4: KM},
                      {0: scores_t, 1: boxes, 2: rec[0], 3: rec[1], 4: rec[2], 5: rec[3], 6: rec[4]},
-                     {0: self.SCORE_THRESH}, {0: self.NMS_THRESH}, name="postprocess.class_nms"))
+                     {0: self.SCORE_THRESH}, {0: self.NMS_THRESH}, name="postprocess.class_nms" + sfx))
             P.add(Op(ops.MERGE_TOPK, {0: B, 1: NS, 2: KM, 3: self.DETS},
-                     {0: rec[0], 1: rec[1], 2: rec[2], 3: rec[3], 4: rec[4], 5: ratio_b, 6: P.out_box,
-                      7: P.out_score, 8: P.out_label, 9: P.out_count}, name="postprocess.merge"))
-        P.input = inp
-        P.cls_logits, P.bbox_regression = cls, reg
-        P.scores_t, P.boxes = scores_t, boxes
-        P.feats = [f[0] for f in feats]
-        return P
+                     {0: rec[0], 1: rec[1], 2: rec[2], 3: rec[3], 4: rec[4], 5: ratio_b, 6: out_box,
+                      7: out_score, 8: out_label, 9: out_count}, name="postprocess.merge" + sfx))
 
 
 # ====================================================================================== FRCNN

@@ -143,6 +143,24 @@ class Buf:
         return flat.view(self.shape)
 
 
+class BufView:
+    """A batch slice of a Buf: images [b0, b0 + n) of a buffer whose leading dimension is the batch
+    (the per-chain inputs / outputs of a batch-split plan)."""
+
+    def __init__(self, buf, b0, n):
+        self.buf, self.b0, self.n = buf, b0, n
+        per = buf.nbytes // buf.shape[0]
+        self.byte_off = b0 * per
+        self.shape = (n,) + tuple(buf.shape[1:])
+        self.dtype = buf.dtype
+
+    def ptr(self):
+        return self.buf.ptr() + self.byte_off
+
+    def tensor(self):
+        return self.buf.tensor()[self.b0:self.b0 + self.n]
+
+
 class Op:
     def __init__(self, kind, i=None, p=None, f=None, d=None, name="", lane=0):
         self.kind, self.name, self.lane = kind, name, lane
@@ -218,7 +236,7 @@ class Plan:
             for j, v in op.p.items():
                 if v is None:
                     rec[k]["p"][j] = 0
-                elif isinstance(v, (Buf, WRef)):
+                elif isinstance(v, (Buf, WRef, BufView)):
                     rec[k]["p"][j] = v.ptr()
                 else:
                     rec[k]["p"][j] = int(v)

@@ -75,3 +75,24 @@ def test_frcnn_detections_match_oracle(frcnn):
         print("frcnn", rep)
         assert rep["n_ref"] > 0 and rep["scores_sorted"]
         assert rep["match_frac"] >= 0.97 and rep["max_box_rel"] <= 1e-3
+
+
+def test_ssd_batch_chains_agree(ssd):
+    """A batch lowered as concurrent sub-batch chains (stream lanes) gives the same detections (tile
+    choices depend on the per-chain batch, so summation orders, not results, may differ)."""
+    from edgeml_amd import synthetic
+    sd, model = ssd
+    imgs = synthetic.make_batch(16, 640, 640, seed=61).cuda()
+    outs = {}
+    for n in (1, 2):
+        model.CHAINS = n
+        model.plans.clear()
+        plan = model.plan(16, 640, 640)
+        assert plan.chains == n
+        got = model(imgs)
+        outs[n] = got
+    model.CHAINS = type(model).CHAINS
+    model.plans.clear()
+    for a, b in zip(outs[1], outs[2]):
+        rep = match_report(a, b, tol=1e-5)
+        assert rep["match_frac"] >= 0.99, rep
