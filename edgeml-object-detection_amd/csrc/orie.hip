@@ -39,6 +39,8 @@ struct OrieApParams {
     const int32_t* lab_cnt;   // [n_img][n_cls] ground-truth boxes per image and class
     const int32_t* target;    // [n_eval] target image of each evaluation
     const int32_t* ens;       // [n_eval][E] ensemble images (target excluded)
+    const uint32_t* wmask;    // mask mode (test.py test_map): [n_eval][bitmap_words] images whose weak
+    const uint32_t* smask;    //   / strong detections take part; null = ORIE mode (target + ensemble)
     double* ap;               // [n_eval][2][n_cls] (weak, strong)
     int32_t* n_l;             // [n_eval][n_cls] labels of the class in the ensemble + target
     int n_cls, E, n_img, bitmap_words;
@@ -75,7 +77,7 @@ __device__ __forceinline__ int block_scan_incl(int v, int* sh, int& total) {
 __global__ void __launch_bounds__(ORIE_NT) orie_ap_kernel(OrieApParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* bitmap = smem;                                      // ensemble membership, n_img bits
-    double* vals = reinterpret_cast<double*>(smem + ((P.bitmap_words + 1) & ~1));  // [2][101]
+    double* vals = reinterpret_cast<double*>(smem + ((2 * P.bitmap_words + 1) & ~1));  // [2][101]
     __shared__ int sh_int[8];
     __shared__ double sh_r[ORIE_NT + 1], sh_e[ORIE_NT + 1];
     __shared__ double sh_carry[2];
@@ -83,35 +85,50 @@ __global__ void __launch_bounds__(ORIE_NT) orie_ap_kernel(OrieApParams P) {
     const int tid = threadIdx.x;
     const int c = (int)(blockIdx.x % (unsigned)P.n_cls);
     const int64_t e = blockIdx.x / (unsigned)P.n_cls;
-    const int img = P.target[e];
-    const int32_t* ens = P.ens + e * P.E;
+    const bool mask_mode = P.wmask != nullptr;
+    const int img = mask_mode ? -1 : P.target[e];
+    uint32_t* sbitmap = bitmap + P.bitmap_words;  // mask mode only (allocated by the launcher)
 
-    for (int w = tid; w < P.bitmap_words; w += ORIE_NT) bitmap[w] = 0u;
-    __syncthreads();
     int nl = 0;
-    for (int s = tid; s < P.E; s += ORIE_NT) {
-        const int im = ens[s];
-        atomicOr(&bitmap[im >> 5], 1u << (im & 31));
-        nl += P.lab_cnt[(int64_t)im * P.n_cls + c];
+    if (mask_mode) {
+        const uint32_t* wm = P.wmask + e * P.bitmap_words;
+        const uint32_t* sm = P.smask + e * P.bitmap_words;
+        for (int w = tid; w < P.bitmap_words; w += ORIE_NT) {
+            bitmap[w] = wm[w];
+            sbitmap[w] = sm[w];
+        }
+        for (int im = tid; im < P.n_img; im += ORIE_NT)
+            if (((wm[im >> 5] | sm[im >> 5]) >> (im & 31)) & 1u) nl += P.lab_cnt[(int64_t)im * P.n_cls + c];
+        __syncthreads();
+    } else {
+        const int32_t* ens = P.ens + e * P.E;
+        for (int w = tid; w < P.bitmap_words; w += ORIE_NT) bitmap[w] = 0u;
+        __syncthreads();
+        for (int s = tid; s < P.E; s += ORIE_NT) {
+            const int im = ens[s];
+            atomicOr(&bitmap[im >> 5], 1u << (im & 31));
+            nl += P.lab_cnt[(int64_t)im * P.n_cls + c];
+        }
     }
-    // n_l = labels of class c over the ensemble plus the target (reward.py:40-41, np.unique counts)
+    // n_l = labels of class c over the evaluated images (reward.py:40-41 / test.py:56, np.unique counts)
     int tot;
     block_scan_incl(nl, sh_int, tot);
-    const int n_l = tot + P.lab_cnt[(int64_t)img * P.n_cls + c];
+    const int n_l = tot + (mask_mode ? 0 : P.lab_cnt[(int64_t)img * P.n_cls + c]);
     if (tid == 0) P.n_l[e * P.n_cls + c] = n_l;
     __syncthreads();
+    auto member = [&](int im, bool strong, int v) -> bool {
+        if (mask_mode) return (((strong ? sbitmap : bitmap)[im >> 5] >> (im & 31)) & 1u) != 0;
+        return strong ? (im == img && v == 1) : (((bitmap[im >> 5] >> (im & 31)) & 1u) || (im == img && v == 0));
+    };
 
     const int64_t s0 = P.seg_off[c], s1 = P.seg_off[c + 1];
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < (mask_mode ? 1 : 2); ++v) {
         double* out = P.ap + (e * 2 + v) * P.n_cls + c;
         // ---- pass 1: members and their TPs
         int np_ = 0, nt_ = 0;
         for (int64_t q = s0 + tid; q < s1; q += ORIE_NT) {
-            const int im = P.ent_img[q];
             const int f = P.ent_flag[q];
-            const bool strong = f & 2;
-            const bool mem = strong ? (im == img && v == 1)
-                                    : (((bitmap[im >> 5] >> (im & 31)) & 1u) || (im == img && v == 0));
+            const bool mem = member(P.ent_img[q], f & 2, v);
             np_ += mem;
             nt_ += mem && (f & 1);
         }
@@ -133,11 +150,8 @@ __global__ void __launch_bounds__(ORIE_NT) orie_ap_kernel(OrieApParams P) {
             const int64_t q = s0 + ch * ORIE_NT + tid;
             bool mem = false, tp = false;
             if (q < s1) {
-                const int im = P.ent_img[q];
                 const int f = P.ent_flag[q];
-                const bool strong = f & 2;
-                mem = strong ? (im == img && v == 1)
-                             : (((bitmap[im >> 5] >> (im & 31)) & 1u) || (im == img && v == 0));
+                mem = member(P.ent_img[q], f & 2, v);
                 tp = mem && (f & 1);
             }
             int cm, ct;
@@ -277,6 +291,27 @@ __global__ void __launch_bounds__(256) box_correct_kernel(BoxCorrectParams P) {
         if (best_det[l] != 0x7fffffff) P.tp[d0 + best_det[l]] = 1;
 }
 
+// lib/data.py:127-160 extract_output_feature for many images: the top-k rows (file order = score
+// order) of each image's detection file -> [num_class + (ncol - 1) * k] float64: per-class counts of the
+// k rows, then the rows' remaining columns flattened.  One thread per image.
+__global__ void output_feature_kernel(const double* __restrict__ rows, const int64_t* __restrict__ off, int n_img,
+                                      int ncol, int num_class, int k, double* __restrict__ out) {
+    const int im = blockIdx.x * blockDim.x + threadIdx.x;
+    if (im >= n_img) return;
+    const int width = num_class + (ncol - 1) * k;
+    double* f = out + (int64_t)im * width;
+    for (int j = 0; j < width; ++j) f[j] = 0.0;
+    const int64_t r0 = off[im];
+    int nr = (int)(off[im + 1] - r0);
+    nr = nr < k ? nr : k;
+    for (int r = 0; r < nr; ++r) {
+        const double* row = rows + (r0 + r) * ncol;
+        const int c = (int)row[0];  // int(data[0]): truncation
+        if (c >= 0 && c < num_class) f[c] += 1.0;
+        for (int q = 1; q < ncol; ++q) f[num_class + r * (ncol - 1) + (q - 1)] = row[q];
+    }
+}
+
 }  // namespace edgedet
 
 using namespace edgedet;
@@ -294,12 +329,12 @@ extern "C" int edgedet_box_correct(const double* det_xyxy, const int32_t* det_cl
     return 0;
 }
 
-extern "C" int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off,
-                               int32_t n_cls, const int32_t* lab_cnt, int64_t n_img, const int32_t* target,
-                               const int32_t* ens, int32_t E, int64_t n_eval, double* ap, int32_t* n_l,
-                               void* stream) {
-    EDGEDET_REQUIRE(seg_off && lab_cnt && target && ap && n_l, "orie_ap: null pointer");
-    EDGEDET_REQUIRE(n_cls > 0 && n_img > 0 && E >= 0 && (E == 0 || ens), "orie_ap: bad sizes");
+static int ap_launch(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off, int32_t n_cls,
+                     const int32_t* lab_cnt, int64_t n_img, const int32_t* target, const int32_t* ens, int32_t E,
+                     const uint32_t* wmask, const uint32_t* smask, int64_t n_eval, double* ap, int32_t* n_l,
+                     void* stream) {
+    EDGEDET_REQUIRE(seg_off && lab_cnt && ap && n_l, "orie_ap: null pointer");
+    EDGEDET_REQUIRE(n_cls > 0 && n_img > 0 && E >= 0, "orie_ap: bad sizes");
     EDGEDET_REQUIRE(n_img <= (1 << 20), "orie_ap: more than 2^20 images (membership bitmap)");
     EDGEDET_REQUIRE(n_eval * n_cls < (1ll << 31), "orie_ap: grid too large");
     if (n_eval == 0) return 0;
@@ -310,6 +345,8 @@ extern "C" int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, 
     P.lab_cnt = lab_cnt;
     P.target = target;
     P.ens = ens;
+    P.wmask = wmask;
+    P.smask = smask;
     P.ap = ap;
     P.n_l = n_l;
     P.n_cls = n_cls;
@@ -317,9 +354,36 @@ extern "C" int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, 
     P.n_img = (int)n_img;
     P.bitmap_words = (int)((n_img + 31) / 32);
     P.n_eval = n_eval;
-    const size_t shm = (size_t)((P.bitmap_words + 1) & ~1) * 4 + 2 * ORIE_GRID * sizeof(double);
+    const size_t shm = (size_t)((2 * P.bitmap_words + 1) & ~1) * 4 + 2 * ORIE_GRID * sizeof(double);
     EDGEDET_REQUIRE(shm <= 150 * 1024, "orie_ap: membership bitmap too large for LDS");
     hipLaunchKernelGGL(orie_ap_kernel, dim3((unsigned)(n_eval * n_cls)), dim3(ORIE_NT), shm, (hipStream_t)stream, P);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off,
+                               int32_t n_cls, const int32_t* lab_cnt, int64_t n_img, const int32_t* target,
+                               const int32_t* ens, int32_t E, int64_t n_eval, double* ap, int32_t* n_l,
+                               void* stream) {
+    EDGEDET_REQUIRE(target && (E == 0 || ens), "orie_ap: null target / ensemble");
+    return ap_launch(ent_img, ent_flag, seg_off, n_cls, lab_cnt, n_img, target, ens, E, nullptr, nullptr, n_eval, ap,
+                     n_l, stream);
+}
+
+extern "C" int edgedet_map_eval(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off,
+                                int32_t n_cls, const int32_t* lab_cnt, int64_t n_img, const uint32_t* weak_mask,
+                                const uint32_t* strong_mask, int64_t n_eval, double* ap, int32_t* n_l, void* stream) {
+    EDGEDET_REQUIRE(weak_mask && strong_mask, "map_eval: null membership masks");
+    return ap_launch(ent_img, ent_flag, seg_off, n_cls, lab_cnt, n_img, nullptr, nullptr, 0, weak_mask, strong_mask,
+                     n_eval, ap, n_l, stream);
+}
+
+extern "C" int edgedet_output_features(const double* rows, const int64_t* off, int64_t n_img, int32_t ncol,
+                                       int32_t num_class, int32_t k, double* out, void* stream) {
+    EDGEDET_REQUIRE(off && out && n_img >= 0 && ncol >= 1 && num_class > 0 && k >= 0, "output_features: bad args");
+    if (n_img == 0) return 0;
+    hipLaunchKernelGGL(output_feature_kernel, dim3((unsigned)cdiv(n_img, 64)), dim3(64), 0, (hipStream_t)stream, rows,
+                       off, (int)n_img, ncol, num_class, k, out);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

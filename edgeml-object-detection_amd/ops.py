@@ -42,7 +42,8 @@ assert OP_DTYPE.itemsize == 8 + 8 * OP_INTS + 8 * OP_PTRS + 8 * OP_DBLS + 4 * OP
 EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
-           "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap")
+           "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
+           "edgedet_map_eval", "edgedet_output_features")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -84,6 +85,8 @@ def lib():
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
     L.edgedet_box_correct.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _dbl, _vp, _i64, _vp]
     L.edgedet_orie_ap.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _vp]
+    L.edgedet_map_eval.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]
+    L.edgedet_output_features.argtypes = [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]
     L.edgedet_conv_tile.argtypes = [_vp]
     L.edgedet_conv_tile.restype = ctypes.c_int
     L.edgedet_conv_weight_k.argtypes = [_i32, _i32, _i64]
@@ -93,7 +96,8 @@ def lib():
     L.edgedet_version.restype = _i32
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
-                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap"):
+                 "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
+           "edgedet_map_eval", "edgedet_output_features"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L

@@ -165,6 +165,23 @@ int edgedet_box_correct(const double* det_xyxy, const int32_t* det_cls, const in
 int edgedet_orie_ap(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off, int32_t n_cls,
                     const int32_t* lab_cnt, int64_t n_img, const int32_t* target, const int32_t* ens, int32_t E,
                     int64_t n_eval, double* ap, int32_t* n_l, void* stream);
+/*
+ * test.py test_map's ap_per_class over a weak/strong mixture (test.py:14-44): evaluation e uses the
+ * weak detections of the images set in weak_mask[e] and the strong detections of those in
+ * strong_mask[e] (bitmaps [n_eval][(n_img + 31) / 32], bit i of word i / 32).  Same entries, AP
+ * layout (ap[e][0][c]) and n_l as edgedet_orie_ap.
+ */
+int edgedet_map_eval(const int32_t* ent_img, const uint8_t* ent_flag, const int64_t* seg_off, int32_t n_cls,
+                     const int32_t* lab_cnt, int64_t n_img, const uint32_t* weak_mask, const uint32_t* strong_mask,
+                     int64_t n_eval, double* ap, int32_t* n_l, void* stream);
+
+/*
+ * lib/data.py:127-160 extract_output_feature for n_img images at once: rows [n][ncol] f64 (each
+ * image's detection-file rows, grouped by off [n_img + 1]); out [n_img][num_class + (ncol - 1) * k]:
+ * class counts of the first k rows, then their columns 1.. flattened (zeros beyond).
+ */
+int edgedet_output_features(const double* rows, const int64_t* off, int64_t n_img, int32_t ncol, int32_t num_class,
+                            int32_t k, double* out, void* stream);
 
 /* --------------------------------------------------------------------------------- misc */
 const char* edgedet_last_error(void);

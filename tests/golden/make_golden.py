@@ -9,6 +9,8 @@ G1 (formatting, torch_models/detect.py:62-105): detect.main() is driven with a s
 G2 (consumer, reward.py + lib/data.py + lib/metrics.py): synthetic weak/strong/label directories are
    fed to set_data(); box_iou / box_correct / ap_per_class / compute_ap / compute_orie (serial,
    np.random.seed(k) before each call) / compute_dcsb outputs are stored.
+G3 (other consumers, on the G2 inputs): test.py test_map with a seeded 3-fold split and two
+   synthetic estimate directories; lib/data.py extract_output_feature(k=25, 80 classes).
 
 Only data (inputs and the reference's outputs) is written: tests/golden/g1_format.npz and
 tests/golden/g2_orie.npz (+ the synthetic input directories packed into g2_inputs.npz).
@@ -229,11 +231,62 @@ def make_g2():
     print("G2:", len(out), "arrays")
 
 
+def make_g3():
+    """G3 (other consumers of the detection files): test.py test_map (realized mAP vs offloading
+    ratio) and lib/data.py extract_output_feature (stage-24 output features), on the G2 inputs."""
+    install_stub([], {})
+    for m in ("lib", "lib.data", "lib.metrics", "reward", "test"):
+        sys.modules.pop(m, None)
+    sys.path.insert(0, REF)
+    import test as ref_test
+    from lib.data import extract_output_feature, set_data
+    sys.path.pop(0)
+    with np.load(os.path.join(HERE, "g2_orie.npz"), allow_pickle=False) as z:
+        g2 = {k: z[k] for k in z.files if k.startswith("in/")}
+    rs = np.random.RandomState(3)
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for k, v in g2.items():
+            _, tag, fname = k.split("/", 2)
+            os.makedirs(os.path.join(td, tag), exist_ok=True)
+            with open(os.path.join(td, tag, fname), "wb") as f:
+                f.write(v.tobytes())
+        weak_d, strong_d, labels = set_data(*(os.path.join(td, t) for t in ("weak", "strong", "labels")))
+        N = len(labels)
+        folds = 3
+        split = np.zeros((folds, N), dtype=bool)
+        perm = rs.permutation(N)
+        for f in range(folds):
+            split[f, perm[f::folds]] = True
+        est_dirs = []
+        for e in range(2):
+            d = os.path.join(td, f"est{e}")
+            os.makedirs(d)
+            for f in range(folds):
+                tr, va = rs.normal(0, 1, int((~split[f]).sum())), rs.normal(0, 1, int(split[f].sum()))
+                np.savez(os.path.join(d, f"estimate{f + 1}.npz"), train_est=tr, val_est=va)
+                out[f"in/est{e}/estimate{f + 1}/train_est"], out[f"in/est{e}/estimate{f + 1}/val_est"] = tr, va
+            est_dirs.append(d)
+        out["in/split"] = split
+        out["test_map"] = ref_test.test_map(weak_d, strong_d, np.concatenate(labels).astype(int), est_dirs, split)
+        feat = os.path.join(td, "features")
+        names = sorted(f[:-4] for f in os.listdir(os.path.join(td, "weak")))
+        for n in names + ["zz_no_output"]:
+            os.makedirs(os.path.join(feat, n))
+        extract_output_feature(os.path.join(td, "weak"), feat, 80, k=25)
+        for n in names + ["zz_no_output"]:
+            out[f"feature/{n}"] = np.load(os.path.join(feat, n, "stage24_output_features.npy"))
+    np.savez_compressed(os.path.join(HERE, "g3_consumers.npz"), **out)
+    print("G3:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     import warnings
     warnings.filterwarnings("ignore")
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
-        make_g1()
-        make_g2()
+        if "--g3-only" not in sys.argv:
+            make_g1()
+            make_g2()
+        make_g3()
     print("done")
