@@ -1034,6 +1034,7 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
     if (rc) return rc;
     tile = conv_resolve_tile(p, tile);
     switch (tile) {
+        case 21: return launch_x6<2, 2, 1, 1>(p, s);  // 64 x 64, bf16x6
         case 22: return launch_x6<2, 2, 2, 1>(p, s);  // 128 x 64, bf16x6
         case 23: return launch_x6<2, 2, 2, 2>(p, s);  // 128 x 128, bf16x6
         case 24: return launch_x6<4, 2, 2, 2>(p, s);  // 256 x 128, bf16x6

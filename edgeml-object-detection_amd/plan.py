@@ -28,6 +28,24 @@ if CONV_MATH not in ("bf16x6", "f32"):
     raise ValueError(f"EDGEDET_CONV_MATH must be 'bf16x6' or 'f32', got {CONV_MATH!r}")
 
 
+# Measured tile per conv shape on gfx950 (tools/tune_conv.py); shapes not listed fall back to the
+# library's heuristic (csrc/conv.hip choose_tile).
+_TILES_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "conv_tiles_gfx950.json")
+CONV_TILES = {}
+if os.path.exists(_TILES_PATH) and os.environ.get("EDGEDET_CONV_TUNED", "1") == "1":
+    import json as _json
+    with open(_TILES_PATH) as _f:
+        CONV_TILES.update(_json.load(_f).get("tiles", {}))
+
+
+def conv_key(op):
+    """Shape key of a CONV op for the tuned tile table."""
+    i = op.i
+    lin = int(i[7] == 1 and i[8] == 1 and i[9] == 1 and i[10] == 0)
+    return ",".join(str(int(v)) for v in (i[0], i[1], i[2], i[3], i[4], i[5], i[6], i[7], i[9], lin,
+                                           int(op.p.get(6) is not None), int(op.p.get(7) is not None)))
+
+
 def _bf16_rn(x):
     """float32 array -> (bf16 bit patterns as uint16, the bf16 values as float32), round to nearest even."""
     u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
@@ -310,5 +328,9 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
          18: (Ho * Wo * yp if y_bstride is None else y_bstride), 19: rH * rW * cout, 20: y_off, 21: rH, 22: rW,
          23: tile, 24: 1 if in_relu else 0}
     w3 = getattr(w, "split", None) if CONV_MATH == "bf16x6" else None
-    return plan.add(Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale, 6: w3, 7: in_shift},
-                       name=name))
+    op = Op(ops.CONV, i, {0: x, 1: w, 2: bias, 3: y, 4: res, 5: in_scale, 6: w3, 7: in_shift}, name=name)
+    if not tile:
+        t = CONV_TILES.get(conv_key(op))
+        if t and (w3 is not None or t < 20):
+            op.i[23] = int(t)
+    return plan.add(op)

