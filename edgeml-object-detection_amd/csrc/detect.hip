@@ -754,6 +754,10 @@ struct ImgSmem {
     int seg_base[KCAP], seg_n[KCAP], seg_next[KCAP];
     int head[SSD_MAXNC];
     int hist[SSD_MAXNC];
+    int coff[SSD_MAXNC];  // class bucket offsets of the round
+    int bucket[M];        // sorted positions grouped by class, score order within a class
+    unsigned long long row[M];  // per candidate: later members of its class it suppresses (bit = rank)
+    int rank[M];          // rank of the candidate within its class bucket
     uint32_t done[PW];
     int wsum[32];
     int red[32];
@@ -799,8 +803,16 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
         rh = ratio[2 * b + 1];
     }
     int total = 0;
+#ifdef NMS_PROFILE
+    long long t_sel = 0, t_sort = 0, t_nms = 0, t_out = 0, tp = __builtin_amdgcn_s_memtime();
+    int rounds = 0;
+#define NMS_STAMP(acc) do { const long long tn = __builtin_amdgcn_s_memtime(); acc += tn - tp; tp = tn; } while (0)
+#else
+#define NMS_STAMP(acc) do { } while (0)
+#endif
     while (true) {
         const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red);
+        NMS_STAMP(t_sel);
         if (m == 0) break;
         for (int t = tid; t < NS; t += NT) S.hist[t] = 0;
         if (tid < m) {
@@ -814,6 +826,7 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             if (kr[j] && ((S.done[i >> 5] >> (i & 31)) & 1u)) kr[j] = 0u;
         }
         bitonic_desc<NT>(S.keys, nullptr, m);
+        NMS_STAMP(t_sort);
         if (tid < m) {
             const int i = key_index(S.keys[tid]);
             const int c = i / topk;
@@ -823,17 +836,114 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             atomicAdd(&S.hist[c], 1);
         }
         __syncthreads();
+        // class buckets: offsets (exclusive scan of the histogram) and each candidate's rank among the
+        // earlier sorted candidates of its class (a broadcast LDS walk), so a class's members are
+        // processed together instead of every class scanning the whole round.
+        if (wv == 0) {
+            int run = 0;
+            for (int c0 = 0; c0 < NS; c0 += 64) {
+                const int c = c0 + lane;
+                const int h = c < NS ? S.hist[c] : 0;
+                int inc = h;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int t2 = __shfl_up(inc, off);
+                    if (lane >= off) inc += t2;
+                }
+                if (c < NS) S.coff[c] = run + inc - h;
+                run += __shfl(inc, 63);
+            }
+        }
+        __syncthreads();
+        if (tid < m) {
+            const int c = S.cls[tid];
+            int r = 0;
+            for (int u = 0; u < tid; ++u) r += S.cls[u] == c ? 1 : 0;
+            S.bucket[S.coff[c] + r] = tid;
+            S.rank[tid] = r;
+        }
+        __syncthreads();
+        // Classes with <= 64 members this round: every candidate builds its suppression row against
+        // the later members of its class (and its flag against the class's earlier kept boxes) in
+        // parallel; then one thread per class runs the greedy scan over those rows.
+        if (tid < m) {
+            const int c = S.cls[tid];
+            const int nc = S.hist[c];
+            if (nc <= 64) {
+                const f32x4 q = S.box[tid];
+                const float aq = (q.z - q.x) * (q.w - q.y);
+                bool alive = true;
+                for (int sg = S.head[c]; sg >= 0 && alive; sg = S.seg_next[sg]) {
+                    const int sb = S.seg_base[sg], sn = S.seg_n[sg];
+                    for (int e = 0; e < sn && alive; ++e) {
+                        const f32x4 kb = S.kbox[sb + e];
+                        const float ka = (kb.z - kb.x) * (kb.w - kb.y);
+                        if (iou_gt(kb, ka, q, aq, iou)) alive = false;
+                    }
+                }
+                unsigned long long row = 0ull;
+                const int* bk = S.bucket + S.coff[c];
+                for (int k2 = S.rank[tid] + 1; k2 < nc; ++k2) {
+                    const f32x4 kb = S.box[bk[k2]];
+                    const float ka = (kb.z - kb.x) * (kb.w - kb.y);
+                    if (iou_gt(q, aq, kb, ka, iou)) row |= 1ull << k2;
+                }
+                S.row[tid] = row;
+                S.kflag[tid] = alive ? 2 : 0;  // 2 = alive candidate, resolved below
+            }
+        }
+        __syncthreads();
+        if (tid < NS) {
+            const int c = tid;
+            const int nc = S.hist[c];
+            if (nc > 0 && nc <= 64) {
+                const int* bk = S.bucket + S.coff[c];
+                unsigned long long removed = 0ull, keptm = 0ull;
+                for (int k2 = 0; k2 < nc; ++k2) {
+                    const int t = bk[k2];
+                    if (S.kflag[t] != 2) removed |= 1ull << k2;
+                }
+                for (int k2 = 0; k2 < nc; ++k2) {
+                    if ((removed >> k2) & 1ull) continue;
+                    keptm |= 1ull << k2;
+                    removed |= S.row[bk[k2]];
+                }
+                const int nk = __popcll(keptm);
+                if (nk) {
+                    const int sb = atomicAdd(&S.misc[0], nk);
+                    const int sg = atomicAdd(&S.misc[1], 1);
+                    int w = 0;
+                    for (int k2 = 0; k2 < nc; ++k2) {
+                        const int t = bk[k2];
+                        if ((keptm >> k2) & 1ull) {
+                            S.kbox[sb + w++] = S.box[t];
+                            S.kflag[t] = 1;
+                        } else {
+                            S.kflag[t] = 0;
+                        }
+                    }
+                    S.seg_base[sg] = sb;
+                    S.seg_n[sg] = nk;
+                    S.seg_next[sg] = S.head[c];
+                    S.head[c] = sg;
+                } else {
+                    for (int k2 = 0; k2 < nc; ++k2) S.kflag[bk[k2]] = 0;
+                }
+            }
+        }
+        __syncthreads();
+        // Classes with more than 64 members this round: one wave per class, 64 members at a time.
         for (int c = wv; c < NS; c += NW) {
-            int remaining = S.hist[c];
-            for (int base = 0; base < m && remaining > 0; base += 64) {
-                const int t = base + lane;
-                const bool in = t < m && S.cls[t] == c;
-                const unsigned long long inm = __ballot(in);
-                if (!inm) continue;
-                remaining -= __popcll(inm);
+            if (S.hist[c] <= 64) continue;
+            const int nc = S.hist[c];
+            for (int base = 0; base < nc; base += 64) {
+                const int j = base + lane;
+                const bool in = j < nc;
+                const int t = in ? S.bucket[S.coff[c] + j] : 0;
                 const f32x4 q = in ? S.box[t] : f32x4{0.f, 0.f, 0.f, 0.f};
                 const float aq = (q.z - q.x) * (q.w - q.y);
                 bool alive = in;
+                // boxes of this class kept in earlier rounds / chunks
                 for (int sg = S.head[c]; sg >= 0 && __ballot(alive); sg = S.seg_next[sg]) {
                     const int sb = S.seg_base[sg], sn = S.seg_n[sg];
                     for (int e = 0; e < sn; ++e) {
@@ -842,20 +952,25 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
                         if (alive && iou_gt(kb, ka, q, aq, iou)) alive = false;
                     }
                 }
-                unsigned long long keptm = 0ull;
-                while (true) {
-                    const unsigned long long am = __ballot(alive);
-                    if (!am) break;
-                    const int l = __builtin_ctzll(am);
-                    keptm |= 1ull << l;
+                // suppression row of each member against the later members of the chunk
+                const int cnt = nc - base < 64 ? nc - base : 64;
+                unsigned long long row = 0ull;
+                for (int k2 = 0; k2 < cnt; ++k2) {
                     f32x4 kb;
-                    kb.x = __shfl(q.x, l);
-                    kb.y = __shfl(q.y, l);
-                    kb.z = __shfl(q.z, l);
-                    kb.w = __shfl(q.w, l);
-                    const float ka = __shfl(aq, l);
-                    if (lane == l) alive = false;
-                    else if (alive && iou_gt(kb, ka, q, aq, iou)) alive = false;
+                    kb.x = __shfl(q.x, k2);
+                    kb.y = __shfl(q.y, k2);
+                    kb.z = __shfl(q.z, k2);
+                    kb.w = __shfl(q.w, k2);
+                    const float ka = __shfl(aq, k2);
+                    if (k2 > lane && in && iou_gt(q, aq, kb, ka, iou)) row |= 1ull << k2;
+                }
+                // greedy in score order over the chunk (scalar: rows read lane by lane)
+                unsigned long long removed = ~__ballot(alive), keptm = 0ull;
+                for (int i = 0; i < cnt; ++i) {
+                    if ((removed >> i) & 1ull) continue;
+                    keptm |= 1ull << i;
+                    removed |= ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(row >> 32), i) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(row & 0xffffffffu), i);
                 }
                 if (keptm) {
                     const int nk = __popcll(keptm);
@@ -881,6 +996,7 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             }
         }
         __syncthreads();
+        NMS_STAMP(t_nms);
         const bool kf = tid < m && S.kflag[tid];
         int tot;
         const int pos = BlockScan<NT>::exclusive(kf ? 1 : 0, S.wsum, tot);
@@ -896,9 +1012,18 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             if (out_label) out_label[o] = (int64_t)(S.cls[tid] + 1);
         }
         total += tot;
+        NMS_STAMP(t_out);
+#ifdef NMS_PROFILE
+        ++rounds;
+#endif
         if (total >= N || m < M) break;
     }
     if (tid == 0) out_count[b] = total < N ? total : N;
+#ifdef NMS_PROFILE
+    if (tid == 0 && b == 0)
+        printf("nms img0: rounds %d total %d select %lld sort %lld nms %lld out %lld (s_memtime ticks)\n", rounds, total,
+               t_sel, t_sort, t_nms, t_out);
+#endif
 }
 
 // ================================================================ RPN per-level selection
