@@ -410,8 +410,78 @@ __global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ h
     }
 }
 
+// Both excitation GEMVs in one launch: one workgroup per SE_FB images does squeeze (mean of the
+// partial sums) -> fc1 + ReLU -> fc2 + Hardsigmoid, so a SqueezeExcitation costs one launch (the
+// latency of the small SSDLite layers, not their bytes, sets their cost).  Used for C * S <= 8192:
+// larger layers read too many weight bytes per workgroup and keep the two-kernel form.
+constexpr int SE_FB = 4;
+__global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__ part, const float* __restrict__ w1,
+                                                      const float* __restrict__ b1, const float* __restrict__ w2t,
+                                                      const float* __restrict__ b2, float* __restrict__ hidden,
+                                                      float* __restrict__ scale, int B, int C, int S, int HW,
+                                                      int parts) {
+    __shared__ float ms[SE_FB * SE_CMAX];
+    __shared__ float hs[SE_FB * SE_SMAX];
+    const int b0 = blockIdx.x * SE_FB;
+    const int nb = min(SE_FB, B - b0);
+    const float inv = 1.f / (float)HW;
+    for (int t = threadIdx.x; t < nb * C; t += 512) {
+        const int bl = t / C, c = t - bl * C;
+        const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
+        float v[SE_PARTS];
+#pragma unroll
+        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)(k < parts ? k : parts - 1) * C];
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < SE_PARTS; ++k) acc += k < parts ? v[k] : 0.f;
+        ms[t] = acc * inv;
+    }
+    __syncthreads();
+    // fc1: output (s, b) by a group of 4 lanes over C quarters (same order as se_fc1_kernel)
+    const int ch = (C + 3) >> 2;
+    for (int o = threadIdx.x >> 2; o < nb * S; o += 128) {
+        const int sl = o / nb, bl = o - sl * nb;
+        const int h = threadIdx.x & 3;
+        const int c0 = h * ch, c1 = min(C, c0 + ch);
+        const float* wr = w1 + (int64_t)sl * C;
+        const float* mr = ms + bl * C;
+        float acc = 0.f;
+        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        if (h == 0) {
+            const float t = acc + b1[sl];
+            hs[bl * S + sl] = t > 0.f ? t : 0.f;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nb * S; t += 512) hidden[(int64_t)b0 * S + t] = hs[t];
+    // fc2: channel c of every image of the group, sequential over S (same order as se_fc2_kernel)
+    for (int c = threadIdx.x; c < C; c += 512) {
+        float a[SE_FB];
+#pragma unroll
+        for (int q = 0; q < SE_FB; ++q) a[q] = 0.f;
+        for (int j = 0; j < S; ++j) {
+            const float wv = w2t[(int64_t)j * C + c];
+#pragma unroll
+            for (int q = 0; q < SE_FB; ++q) a[q] = fmaf(wv, hs[q * S + j], a[q]);
+        }
+        const float bias = b2[c];
+#pragma unroll
+        for (int q = 0; q < SE_FB; ++q)
+            if (q < nb) scale[(int64_t)(b0 + q) * C + c] = apply_act(a[q] + bias, ACT_HSIGMOID);
+    }
+}
+
 int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
                  float* hidden, float* scale, int B, int C, int S, int HW, int parts, hipStream_t s) {
+    if ((int64_t)C * S <= 8192 && parts >= 1 && parts <= SE_PARTS && S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX) {
+        EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
+        hipLaunchKernelGGL(se_fused_kernel, dim3((unsigned)cdiv(B, SE_FB)), dim3(512), 0, s, part, w1, b1, w2t, b2,
+                           hidden, scale, B, C, S, HW, parts);
+        EDGEDET_LAUNCH_CHECK();
+        return 0;
+    }
     EDGEDET_REQUIRE(parts >= 1 && parts <= SE_PARTS, "se_fc: 1..16 squeeze partial sums");
     EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
     EDGEDET_REQUIRE(S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX && HW >= 1, "se_fc: C <= 1024, S <= 512");
