@@ -313,49 +313,111 @@ __device__ __forceinline__ int block_sum_uniform(int wave_val, int* red) {
     return tot;
 }
 
+// count of keys >= t over the block.  red holds 2 x NW slots used alternately by successive calls
+// (`parity`), so one barrier per probe suffices: a wave cannot rewrite a slot set before every wave
+// has passed the barrier that follows the next probe's write.
 template <int NT, int PER>
-__device__ __forceinline__ int count_ge(const uint32_t (&kr)[PER], uint32_t t, int* red) {
+__device__ __forceinline__ int count_ge(const uint32_t (&kr)[PER], uint32_t t, int* red, int& parity) {
+    constexpr int NW = NT / 64;
     int c = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) c += __popcll(__ballot(kr[j] >= t));
-    return block_sum_uniform<NT>(c, red);
+    int* r = red + parity * NW;
+    parity ^= 1;
+    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = c;
+    __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += r[w];
+    return tot;
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, int* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
+        v = u > v ? u : v;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (int)v;
+    __syncthreads();
+    uint32_t m = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) m = (uint32_t)red[w] > m ? (uint32_t)red[w] : m;
+    __syncthreads();
+    return m;
 }
 
 template <int NT, int PER>
 __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsigned long long* keys, int* wsum,
                                 int* red, bool all_ties = false) {
-    const int nvalid = count_ge<NT, PER>(kr, 1u, red);
+    int parity = 0;
+    const int nvalid = count_ge<NT, PER>(kr, 1u, red, parity);
     uint32_t T = 1u;
     int need_eq = 0;
     const bool take_all = nvalid <= K;
     if (!take_all) {
-        uint64_t lo = 1, hi = 1ull << 32;  // count(>= lo) >= K > count(>= hi)
+        uint32_t km = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) km = kr[j] > km ? kr[j] : km;
+        // bisection on [1, max + 1): count(>= lo) >= K > count(>= hi)
+        uint64_t lo = 1, hi = (uint64_t)block_max_u32<NT>(km, red + 2 * (NT / 64)) + 1;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (count_ge<NT, PER>(kr, (uint32_t)mid, red) >= K) lo = mid;
+            if (count_ge<NT, PER>(kr, (uint32_t)mid, red, parity) >= K) lo = mid;
             else hi = mid;
         }
         T = (uint32_t)lo;
-        const int greater = (hi >> 32) ? 0 : count_ge<NT, PER>(kr, (uint32_t)hi, red);
+        const int greater = (hi >> 32) ? 0 : count_ge<NT, PER>(kr, (uint32_t)hi, red, parity);
         need_eq = all_ties ? cap : K - greater;
     }
-    int written = 0, eq_taken = 0;
+    __syncthreads();
+    // Compaction.  Callers sort the selected keys, so keys > T go out in any order: one scan of
+    // per-thread counts.  Ties == T are taken whole when they fit the budget; otherwise the first
+    // need_eq of them in index order (element i = threadIdx.x + NT * j), with per-register scans.
+    int ngt = 0, neq = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t k = kr[j];
-        const bool gt = take_all ? (k >= 1u) : (k > T);
-        const bool eq = !take_all && k == T;
-        int tot_gt, tot_eq;
-        const int pos_gt = BlockScan<NT>::exclusive(gt ? 1 : 0, wsum, tot_gt);
-        const int pos_eq = BlockScan<NT>::exclusive(eq ? 1 : 0, wsum, tot_eq);
-        const int budget = need_eq - eq_taken;
-        const uint32_t i = threadIdx.x + (uint32_t)NT * j;
-        if (gt && written + pos_gt < cap) keys[written + pos_gt] = make_key(k, i);
-        if (eq && pos_eq < budget && written + tot_gt + pos_eq < cap)
-            keys[written + tot_gt + pos_eq] = make_key(k, i);
-        const int eq_used = tot_eq < budget ? tot_eq : (budget > 0 ? budget : 0);
-        written += tot_gt + eq_used;
-        eq_taken += eq_used;
+        ngt += (take_all ? (k >= 1u) : (k > T)) ? 1 : 0;
+        neq += (!take_all && k == T) ? 1 : 0;
+    }
+    int tot_gt, tot_eq;
+    int w = BlockScan<NT>::exclusive_sum(ngt, wsum, tot_gt);
+    const int pos_eq = BlockScan<NT>::exclusive_sum(neq, wsum, tot_eq);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t k = kr[j];
+        if (take_all ? (k >= 1u) : (k > T)) {
+            if (w < cap) keys[w] = make_key(k, threadIdx.x + (uint32_t)NT * j);
+            ++w;
+        }
+    }
+    int written = tot_gt;
+    if (tot_eq <= need_eq) {
+        int e = tot_gt + pos_eq;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t k = kr[j];
+            if (!take_all && k == T) {
+                if (e < cap) keys[e] = make_key(k, threadIdx.x + (uint32_t)NT * j);
+                ++e;
+            }
+        }
+        written += tot_eq;
+    } else if (need_eq > 0) {
+        int eq_taken = 0;
+        for (int j = 0; j < PER; ++j) {
+            const bool eq = kr[j] == T;
+            int tj;
+            const int pe = BlockScan<NT>::exclusive(eq ? 1 : 0, wsum, tj);
+            const int budget = need_eq - eq_taken;
+            if (eq && pe < budget && written + eq_taken + pe < cap)
+                keys[written + eq_taken + pe] = make_key(kr[j], threadIdx.x + (uint32_t)NT * j);
+            eq_taken += tj < budget ? tj : (budget > 0 ? budget : 0);
+            if (eq_taken >= need_eq) break;
+        }
+        written += eq_taken;
     }
     __syncthreads();
     return written < cap ? written : cap;
