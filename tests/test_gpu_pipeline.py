@@ -80,6 +80,21 @@ def test_detect_cli_voc_model_path_matches_oracle(model, kind):
         _match_files(out, os.path.join(td, "oracle"), 0.97)
 
 
+def test_pipeline_module_runs_config4_in_miniature():
+    """edgeml_amd.pipeline: weak + strong detection files, then ORIE, in one process."""
+    from edgeml_amd import pipeline, synthetic
+    warnings.filterwarnings("ignore")
+    with tempfile.TemporaryDirectory() as td:
+        img, lab, work = (os.path.join(td, d) for d in ("imgs", "labels", "work"))
+        synthetic.make_dataset(img, 5, seed=2, label_dir=lab)
+        pipeline.main(pipeline.getargs([img, lab, work, "--num-ensemble", "3"]))
+        for d in ("weak", "strong"):
+            assert sorted(os.listdir(os.path.join(work, d))) == [f"{i:012d}.npy" for i in range(5)]
+        with np.load(os.path.join(work, "reward", "orie3.npz")) as z:
+            r = z["reward"]
+        assert r.shape == (5,) and np.all(np.isfinite(r))
+
+
 def test_detect_then_reward_cli_equals_oracle_pipeline():
     from edgeml_amd import detect, reward, synthetic
     from oracle import orie
