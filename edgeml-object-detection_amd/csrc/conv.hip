@@ -464,22 +464,28 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK6 = 16;
 constexpr int LDR6 = 24;  // padded LDS row, in bf16
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned bf16_pk(f32x2 v) {  // one v_cvt_pk_bf16_f32 (RN) for two values
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 bf16_unpk(unsigned u) {
+    return f32x2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+// x = hi + mid + lo (RN at each step), computed on element pairs: 6 packed converts, 8 unpacks and
+// 4 two-wide subtractions per f32x4.
 __device__ __forceinline__ void split3_bf16(const f32x4& v, u16x4& h, u16x4& m, u16x4& l) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float x = v[e];
-        const __bf16 x0 = (__bf16)x;
-        const float r1 = x - (float)x0;
-        const __bf16 x1 = (__bf16)r1;
-        const float r2 = r1 - (float)x1;
-        const __bf16 x2 = (__bf16)r2;
-        h[e] = __builtin_bit_cast(unsigned short, x0);
-        m[e] = __builtin_bit_cast(unsigned short, x1);
-        l[e] = __builtin_bit_cast(unsigned short, x2);
-    }
+    const f32x2 a{v.x, v.y}, b{v.z, v.w};
+    const unsigned ha = bf16_pk(a), hb = bf16_pk(b);
+    const f32x2 ra = a - bf16_unpk(ha), rb = b - bf16_unpk(hb);
+    const unsigned ma = bf16_pk(ra), mb = bf16_pk(rb);
+    const f32x2 sa = ra - bf16_unpk(ma), sb = rb - bf16_unpk(mb);
+    h = __builtin_bit_cast(u16x4, uint2{ha, hb});
+    m = __builtin_bit_cast(u16x4, uint2{ma, mb});
+    l = __builtin_bit_cast(u16x4, uint2{bf16_pk(sa), bf16_pk(sb)});
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, bool XF, bool UT>
 __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     constexpr int NT = WM * WN * 64;
     constexpr int BM = WM * TM * 32;
@@ -521,7 +527,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
         const int row = (tid >> 2) + (NT / 4) * j;
         const int m = m0 + row;
         if (m < p.M && p.lin_x) {
-            a_b[j] = (p.in_scale || p.in_shift) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_b[j] = XF ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * p.x_pstride;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
@@ -561,7 +567,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     }
     // Cin % 16 == 0: a 16-wide K stage never crosses a filter tap, so the tap of a stage is
     // wavefront-uniform (scalar) and a thread's A address is its row pointer plus a uniform offset.
-    const bool uniform_tap = (p.Cin & 15) == 0;
 
     struct Regs {
         f32x4 a[AJ];
@@ -570,7 +575,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     Regs r0, r1;
 
     auto load_stage = [&](Regs& R, int k0) {
-        if (uniform_tap) {
+        if constexpr (UT) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);
             const int ci = k0 - tap * p.Cin + c4 * 4;
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
@@ -582,7 +587,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (kval && (unsigned)(a_ih0[j] + kh) < (unsigned)p.H && (unsigned)(a_iw0[j] + kw) < (unsigned)p.W) {
                     v = *reinterpret_cast<const f32x4*>(a_row[j] + off);
-                    v = in_transform(p, v, a_b[j], ci);
+                    if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
             }
@@ -599,14 +604,15 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
                     v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                    v = in_transform(p, v, a_b[j], ci);
+                    if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
             }
         }
 #pragma unroll
         for (int j = 0; j < BJ; ++j)
-            R.b[j] = b_ok[j] ? *reinterpret_cast<const uint4*>(b_row[j] + k0) : uint4{0u, 0u, 0u, 0u};
+            R.b[j] = (BL % NT == 0 || tid + NT * j < BL) ? *reinterpret_cast<const uint4*>(b_row[j] + k0)
+                                                       : uint4{0u, 0u, 0u, 0u};  // rows past Cout: row 0
     };
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
@@ -713,6 +719,9 @@ constexpr int BK6B = 32;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
 
+// XF: the input transform is active (SE scale / GN shift / ReLU); UT: Cin % 32 == 0, so every stage
+// lies inside one filter tap and the tap decomposition is wave-uniform (scalar) work.
+template <bool XF, bool UT>
 __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     constexpr int WM = 4, WN = 2, TM = 2, TN = 2, NT = 512;
     constexpr int BM = 256, BN = 128;
@@ -748,7 +757,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     for (int j = 0; j < AJ; ++j) {
         const int m = m0 + (tid >> 3) + (NT / 8) * j;
         if (m < p.M && p.lin_x) {
-            a_b[j] = (p.in_scale || p.in_shift) ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+            a_b[j] = XF ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * p.x_pstride;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
@@ -758,9 +767,11 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             const int oh = (int)fdiv((uint32_t)rem, p.div_wo);
             const int ow = rem - oh * p.Wo;
             a_b[j] = b;
-            a_base[j] = (int64_t)b * p.x_bstride;
             a_ih0[j] = oh * p.stride - p.pad;
             a_iw0[j] = ow * p.stride - p.pad;
+            // UT: fold the window origin into the base (the tap offset is added per stage)
+            a_base[j] = (int64_t)b * p.x_bstride +
+                        (UT ? (int64_t)(a_ih0[j] * p.W + a_iw0[j]) * p.x_pstride : 0);
         } else {
             a_b[j] = 0;
             a_base[j] = 0;
@@ -778,21 +789,39 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     f32x4 ra[AJ];
     uint4 rb[3];
     auto load_stage = [&](int k0) {
-        const int k = k0 + c8 * 4;
-        const int tap = (int)fdiv((uint32_t)k, p.div_cin);
-        const int ci = k - tap * p.Cin;
-        const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
-        const int kw = tap - kh * p.KW;
-        const bool kval = tap < KHW;
+        if constexpr (UT) {
+            const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
+            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+            const int kw = tap - kh * p.KW;
+            const int ci = k0 - tap * p.Cin + c8 * 4;
+            const float* xt = p.x + (int64_t)(kh * p.W + kw) * p.x_pstride + ci;
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
-            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
-                v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
-                v = in_transform(p, v, a_b[j], ci);
+            for (int j = 0; j < AJ; ++j) {
+                const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+                if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                    v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
+                    if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
+                }
+                ra[j] = v;
             }
-            ra[j] = v;
+        } else {
+            const int k = k0 + c8 * 4;
+            const int tap = (int)fdiv((uint32_t)k, p.div_cin);
+            const int ci = k - tap * p.Cin;
+            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+            const int kw = tap - kh * p.KW;
+            const bool kval = tap < KHW;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (kval && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                    v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
+                    if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
+                }
+                ra[j] = v;
+            }
         }
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
@@ -901,7 +930,10 @@ static int launch_x6b(const ConvParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
     const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
-    hipLaunchKernelGGL(conv_x6b_kernel, dim3((unsigned)nwg), dim3(512), 0, s, p);
+    const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
+    auto k = xf ? (ut ? conv_x6b_kernel<true, true> : conv_x6b_kernel<true, false>)
+                : (ut ? conv_x6b_kernel<false, true> : conv_x6b_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -928,7 +960,10 @@ static int launch_x6(const ConvParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.Kpad % BK6 == 0, "conv bf16x6: Kpad must be a multiple of 16");
     const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, BN);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
-    hipLaunchKernelGGL((conv_x6_kernel<WM, WN, TM, TN>), dim3((unsigned)nwg), dim3(WM * WN * 64), 0, s, p);
+    const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = (p.Cin & 15) == 0;
+    auto k = xf ? (ut ? conv_x6_kernel<WM, WN, TM, TN, true, true> : conv_x6_kernel<WM, WN, TM, TN, true, false>)
+                : (ut ? conv_x6_kernel<WM, WN, TM, TN, false, true> : conv_x6_kernel<WM, WN, TM, TN, false, false>);
+    hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(WM * WN * 64), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
