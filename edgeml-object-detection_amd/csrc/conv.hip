@@ -15,6 +15,7 @@
 // wave contributes k = 16h + 8q + t (q, t loop indices), so both operands are read from LDS as
 // contiguous f32x4s (ds_read_b128) from K-contiguous rows padded to 36 floats (conflict-free
 // for the b128 lane groups).
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.hpp"
@@ -474,6 +475,10 @@ __device__ __forceinline__ f32x2 bf16_unpk(unsigned u) {
 }
 // x = hi + mid + lo (RN at each step), computed on element pairs: 6 packed converts, 8 unpacks and
 // 4 two-wide subtractions per f32x4.
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u16x8 u16x8_of(u16x4 a, u16x4 b) {
+    return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 __device__ __forceinline__ void split3_bf16(const f32x4& v, u16x4& h, u16x4& m, u16x4& l) {
     const f32x2 a{v.x, v.y}, b{v.z, v.w};
     const unsigned ha = bf16_pk(a), hb = bf16_pk(b);
@@ -709,11 +714,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 // row bits 2..3 (chunk' = chunk ^ ((row >> 2) & 3)): the four lane groups of a ds_read_b128 then hit
 // 16 distinct 16-B slots of the 256-B bank row (conflict-free), and the double-buffered image of the
 // three A and three B planes fits 144 KiB (one block of 8 waves per CU, two waves per SIMD).
-#ifndef X6_T14
-#define X6_T14 0
+#ifndef X6B_PF
+#define X6B_PF 1
 #endif
-#ifndef X6_PRIO
-#define X6_PRIO 0
+#ifndef X6B_PIPE
+#define X6B_PIPE 1
 #endif
 constexpr int BK6B = 32;
 
@@ -721,11 +726,16 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 
 // XF: the input transform is active (SE scale / GN shift / ReLU); UT: Cin % 32 == 0, so every stage
 // lies inside one filter tap and the tap decomposition is wave-uniform (scalar) work.
-template <bool XF, bool UT>
+// PS: the input arrives pre-split (p.x3: three dense bf16 planes written by split_act_kernel, input
+// transform already applied), so a stage is 2 rows x 3 planes of 16-B loads per thread, stored to
+// LDS unchanged (requires UT, !XF).
+template <bool XF, bool UT, bool PS>
 __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
+    static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     constexpr int WM = 4, WN = 2, TM = 2, TN = 2, NT = 512;
     constexpr int BM = 256, BN = 128;
-    constexpr int AJ = BM * BK6B / 4 / NT;  // 4 f32x4 A loads per thread per stage
+    constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
+    constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
     constexpr int PA = BM * BK6B, PB = BN * BK6B;  // bf16 elements per plane
     static_assert(3 * BN * BK6B / 8 == 3 * NT, "one B-plane chunk per thread per plane");
 
@@ -751,14 +761,18 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int n0 = (bid % nnt) * BN;
 
     const int c8 = tid & 7;  // f32x4 column of the 32-deep stage
+    const int a_row0 = PS ? tid >> 2 : tid >> 3;
+    // pixel / batch strides of the A source: the fp32 input, or the dense bf16 planes
+    const int x_ps = PS ? p.Cin : p.x_pstride;
+    const int64_t x_bs = PS ? (int64_t)p.H * p.W * p.Cin : p.x_bstride;
     int64_t a_base[AJ];
     int a_ih0[AJ], a_iw0[AJ], a_b[AJ];
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
-        const int m = m0 + (tid >> 3) + (NT / 8) * j;
+        const int m = m0 + a_row0 + AROWS * j;
         if (m < p.M && p.lin_x) {
             a_b[j] = XF ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
-            a_base[j] = (int64_t)m * p.x_pstride;
+            a_base[j] = (int64_t)m * x_ps;
             a_ih0[j] = 0;
             a_iw0[j] = 0;
         } else if (m < p.M) {
@@ -770,8 +784,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             a_ih0[j] = oh * p.stride - p.pad;
             a_iw0[j] = ow * p.stride - p.pad;
             // UT: fold the window origin into the base (the tap offset is added per stage)
-            a_base[j] = (int64_t)b * p.x_bstride +
-                        (UT ? (int64_t)(a_ih0[j] * p.W + a_iw0[j]) * p.x_pstride : 0);
+            a_base[j] = (int64_t)b * x_bs + (UT ? (int64_t)(a_ih0[j] * p.W + a_iw0[j]) * x_ps : 0);
         } else {
             a_b[j] = 0;
             a_base[j] = 0;
@@ -786,10 +799,28 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const unsigned short* b_src = reinterpret_cast<const unsigned short*>(p.w3) +
                                   (int64_t)(b_ok ? n0 + b_row : 0) * p.Kpad + 8 * b_chunk;
 
-    f32x4 ra[AJ];
-    uint4 rb[3];
-    auto load_stage = [&](int k0) {
-        if constexpr (UT) {
+    struct Regs {
+        f32x4 a[PS ? 1 : AJ];
+        uint4 a3[PS ? AJ : 1][3];
+        uint4 b[3];
+    };
+    const int64_t x3plane = (int64_t)p.B * p.H * p.W * p.Cin;
+    auto load_stage = [&](Regs& R, int k0) {
+        if constexpr (PS) {
+            const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
+            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
+            const int kw = tap - kh * p.KW;
+            const unsigned short* xt = reinterpret_cast<const unsigned short*>(p.x3) +
+                                       (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin) + 8 * (tid & 3);
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    R.a3[j][pl] = ok ? *reinterpret_cast<const uint4*>(xt + pl * x3plane + a_base[j]) : uint4{0u, 0u, 0u, 0u};
+            }
+        } else if constexpr (UT) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
             const int kw = tap - kh * p.KW;
@@ -803,7 +834,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
                     v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
                     if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
-                ra[j] = v;
+                R.a[j] = v;
             }
         } else {
             const int k = k0 + c8 * 4;
@@ -820,29 +851,38 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
                     v = *reinterpret_cast<const f32x4*>(p.x + a_base[j] + (int64_t)(ih * p.W + iw) * p.x_pstride + ci);
                     if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
-                ra[j] = v;
+                R.a[j] = v;
             }
         }
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-            rb[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
+            R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
     };
-    auto store_stage = [&](int buf) {
+    auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
+        if constexpr (PS) {
 #pragma unroll
-        for (int j = 0; j < AJ; ++j) {
-            const int row = (tid >> 3) + (NT / 8) * j;
-            u16x4 h, m, l;
-            split3_bf16(ra[j], h, m, l);
-            const int o = swz64(row, c8 >> 1) + 4 * (c8 & 1);
-            *reinterpret_cast<u16x4*>(A + 0 * PA + o) = h;
-            *reinterpret_cast<u16x4*>(A + 1 * PA + o) = m;
-            *reinterpret_cast<u16x4*>(A + 2 * PA + o) = l;
+            for (int j = 0; j < AJ; ++j) {
+                const int o = swz64(a_row0 + AROWS * j, tid & 3);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(A + pl * PA + o) = R.a3[j][pl];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                const int row = a_row0 + AROWS * j;
+                u16x4 h, m, l;
+                split3_bf16(R.a[j], h, m, l);
+                const int o = swz64(row, c8 >> 1) + 4 * (c8 & 1);
+                *reinterpret_cast<u16x4*>(A + 0 * PA + o) = h;
+                *reinterpret_cast<u16x4*>(A + 1 * PA + o) = m;
+                *reinterpret_cast<u16x4*>(A + 2 * PA + o) = l;
+            }
         }
         const int o = swz64(b_row, b_chunk);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = rb[pl];
+        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = R.b[pl];
     };
 
     floatx16 acc[TM][TN];
@@ -856,73 +896,152 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int nk = p.Kpad / BK6B;
     const int h = lane >> 5;
     const int l32 = lane & 31;
-    auto compute = [&](int buf) {
+    struct Frags {
+        bf16x8 a[TM][3], b[TN][3];
+    };
+    // Fragments of K half s (16 of the stage's 32) of LDS buffer buf.
+    auto read_frags = [&](Frags& F, int buf, int s) {
         const unsigned short* A = As + buf * 3 * PA;
         const unsigned short* Bb = Bs + buf * 3 * PB;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bf16x8 af[TM][3], bfr[TN][3];
+        for (int i = 0; i < TM; ++i) {
+            const int o = swz64(wave_m * TM * 32 + i * 32 + l32, 2 * s + h);
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int o = swz64(wave_m * TM * 32 + i * 32 + l32, 2 * s + h);
+            for (int pl = 0; pl < 3; ++pl) F.a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * PA + o);
+        }
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * PA + o);
-            }
+        for (int j = 0; j < TN; ++j) {
+            const int o = swz64(wave_n * TN * 32 + j * 32 + l32, 2 * s + h);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int o = swz64(wave_n * TN * 32 + j * 32 + l32, 2 * s + h);
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
-            }
-#if X6_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
-                }
-#if X6_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
+            for (int pl = 0; pl < 3; ++pl) F.b[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
         }
     };
-#if X6_T14
-    // Write-after-barrier: the registers loaded during stage k-1 are split and stored into the free
-    // buffer at the top of stage k, then stage k+2's loads are issued and stage k's MFMAs run.
-    load_stage(0);
-    store_stage(0);
-    if (nk > 1) load_stage(BK6B);
-    __syncthreads();
-    for (int kc = 0; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < nk) {
-            store_stage(buf ^ 1);
-            if (kc + 2 < nk) load_stage((kc + 2) * BK6B);
+    // smallest terms first: (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
+    auto mfmas = [&](const Frags& F) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][2], F.b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][1], F.b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][1], F.b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][0], acc[i][j], 0, 0, 0);
+            }
+    };
+    auto compute = [&](int buf) {
+        Frags F;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            read_frags(F, buf, s);
+            mfmas(F);
         }
-        compute(buf);
+    };
+#if X6B_PIPE
+    // Skewed pipeline: the second K half of stage k-1 (fragments held in registers across the
+    // barrier) runs while stage k's first-half fragments are read, and stage k+1's operands are
+    // written to the other buffer under stage k's MFMAs, so the matrix pipe does not idle through
+    // the read latency after each barrier.
+    Regs r0;
+    Frags F0, F1;
+    load_stage(r0, 0);
+    store_stage(r0, 0);
+    __syncthreads();
+    if (nk > 1) load_stage(r0, BK6B);
+    read_frags(F0, 0, 0);
+    mfmas(F0);
+    read_frags(F1, 0, 1);
+    if (nk > 1) store_stage(r0, 1);
+    __syncthreads();
+#ifndef X6B_DIAG
+#define X6B_DIAG 0  // timing ablations (wrong results): 1 no barrier, 2 no global loads, 4 no LDS reads, 8 no LDS writes
+#endif
+    for (int kc = 1; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        if (!(X6B_DIAG & 2) && kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B);
+        if (!(X6B_DIAG & 4)) read_frags(F0, buf, 0);
+        __builtin_amdgcn_sched_barrier(0);  // issue the reads before the MFMAs that hide them
+        mfmas(F1);
+#if X6B_PIPE == 2
+        if (!(X6B_DIAG & 8)) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+        mfmas(F0);
+        if (!(X6B_DIAG & 4)) read_frags(F1, buf, 1);
+#else
+        mfmas(F0);
+        if (!(X6B_DIAG & 4)) read_frags(F1, buf, 1);
+        if (!(X6B_DIAG & 8)) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+#endif
+        if (!(X6B_DIAG & 1)) __syncthreads();
+    }
+    mfmas(F1);
+#elif X6B_PF == 2
+    // Two register stages: stage k+2's global loads are issued before stage k's MFMAs, stage k+1's
+    // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
+    // time to land.
+    Regs r0, r1;
+    load_stage(r0, 0);
+    store_stage(r0, 0);
+    if (nk > 1) load_stage(r1, BK6B);
+    __syncthreads();
+    auto step = [&](int kc, Regs& hold, Regs& next) {
+        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6B);
+        compute(kc & 1);
+        if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
         __syncthreads();
+    };
+    for (int kc = 0; kc < nk; kc += 2) {
+        step(kc, r1, r0);
+        if (kc + 1 < nk) step(kc + 1, r0, r1);
     }
 #else
-    load_stage(0);
-    store_stage(0);
+    Regs r0;
+    load_stage(r0, 0);
+    store_stage(r0, 0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage((kc + 1) * BK6B);
+        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B);
         compute(buf);
-        if (kc + 1 < nk) store_stage(buf ^ 1);
+        if (kc + 1 < nk) store_stage(r0, buf ^ 1);
         __syncthreads();
     }
 #endif
 
     conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+}
+
+// Pre-split of a conv input for the PS tile: out[pl][pix][c] (three dense bf16 planes, the RN split
+// of split3_bf16) of transform(x[pix][c]); 8 channels per thread, a grid-stride pass.  HBM-bound:
+// 4 B read + 6 B written per element.
+template <bool XF>
+__global__ void __launch_bounds__(256) split_act_kernel(ConvParams p) {
+    const int C8 = p.Cin >> 3;
+    const int64_t HW = (int64_t)p.H * p.W, npix = (int64_t)p.B * HW, n = npix * C8;
+    unsigned short* out = reinterpret_cast<unsigned short*>(p.x3);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t pix = i / C8;
+        const int c = (int)(i - pix * C8) * 8;
+        const int64_t b = pix / HW;
+        const float* src = p.x + b * p.x_bstride + (pix - b * HW) * p.x_pstride + c;
+        f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+        if constexpr (XF) {
+            v0 = in_transform(p, v0, (int)b, c);
+            v1 = in_transform(p, v1, (int)b, c + 4);
+        }
+        u16x4 h0, m0, l0, h1, m1, l1;
+        split3_bf16(v0, h0, m0, l0);
+        split3_bf16(v1, h1, m1, l1);
+        unsigned short* d = out + pix * p.Cin + c;
+        const int64_t plane = npix * p.Cin;
+        *reinterpret_cast<uint4*>(d) = __builtin_bit_cast(uint4, u16x8_of(h0, h1));
+        *reinterpret_cast<uint4*>(d + plane) = __builtin_bit_cast(uint4, u16x8_of(m0, m1));
+        *reinterpret_cast<uint4*>(d + 2 * plane) = __builtin_bit_cast(uint4, u16x8_of(l0, l1));
+    }
+}
+
+static bool x6b_presplit(const ConvParams& p) {
+    return p.x3 && p.Cin % BK6B == 0 && p.x_pstride % 4 == 0 && ((uintptr_t)p.x3 & 15) == 0;
 }
 
 static int launch_x6b(const ConvParams& p, hipStream_t s) {
@@ -931,8 +1050,17 @@ static int launch_x6b(const ConvParams& p, hipStream_t s) {
     const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
     const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
-    auto k = xf ? (ut ? conv_x6b_kernel<true, true> : conv_x6b_kernel<true, false>)
-                : (ut ? conv_x6b_kernel<false, true> : conv_x6b_kernel<false, false>);
+    if (x6b_presplit(p)) {
+        const int64_t items = (int64_t)p.B * p.H * p.W * (p.Cin / 8);
+        const unsigned g = (unsigned)std::min<int64_t>(cdiv(items, 256), 256 * 64);
+        hipLaunchKernelGGL(xf ? split_act_kernel<true> : split_act_kernel<false>, dim3(g), dim3(256), 0, s, p);
+        EDGEDET_LAUNCH_CHECK();
+        hipLaunchKernelGGL((conv_x6b_kernel<false, true, true>), dim3((unsigned)nwg), dim3(512), 0, s, p);
+        EDGEDET_LAUNCH_CHECK();
+        return 0;
+    }
+    auto k = xf ? (ut ? conv_x6b_kernel<true, true, false> : conv_x6b_kernel<true, false, false>)
+                : (ut ? conv_x6b_kernel<false, true, false> : conv_x6b_kernel<false, false, false>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
@@ -1118,12 +1246,13 @@ extern "C" int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, vo
     return 0;
 }
 
-extern "C" int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
-                                 const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH, int32_t KW,
-                                 int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
-                                 void* stream) {
+extern "C" int edgedet_conv2d_x3(const float* x, uint16_t* x3, int64_t B, int64_t H, int64_t W, int64_t Cin,
+                                 const float* w, const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH,
+                                 int32_t KW, int32_t stride, int32_t pad, int32_t act, const float* res, float* y,
+                                 int32_t tile, void* stream) {
     ConvParams p{};
     p.w3 = w3;
+    p.x3 = x3;
     p.x = x;
     p.w = w;
     p.bias = bias;
@@ -1151,6 +1280,14 @@ extern "C" int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W
     p.res_pstride = (int)Cout;
     p.res_bstride = p.y_bstride;
     return conv_launch(p, tile, (hipStream_t)stream);
+}
+
+extern "C" int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,
+                                 const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH, int32_t KW,
+                                 int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
+                                 void* stream) {
+    return edgedet_conv2d_x3(x, nullptr, B, H, W, Cin, w, w3, bias, Cout, KH, KW, stride, pad, act, res, y, tile,
+                             stream);
 }
 
 extern "C" int edgedet_conv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w,

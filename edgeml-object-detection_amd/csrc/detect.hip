@@ -348,9 +348,12 @@ __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, int* red) {
     return m;
 }
 
+// kmin < K relaxes the selection to "some prefix of the order": the bisection stops at the first
+// probe t with kmin <= count(>= t) <= K and every key >= t is taken (ties whole), which is all a
+// caller that consumes candidates in global order, round by round, needs.
 template <int NT, int PER>
 __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsigned long long* keys, int* wsum,
-                                int* red, bool all_ties = false) {
+                                int* red, bool all_ties = false, int kmin = -1) {
     int parity = 0;
     const int nvalid = count_ge<NT, PER>(kr, 1u, red, parity);
     uint32_t T = 1u;
@@ -362,14 +365,26 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
         for (int j = 0; j < PER; ++j) km = kr[j] > km ? kr[j] : km;
         // bisection on [1, max + 1): count(>= lo) >= K > count(>= hi)
         uint64_t lo = 1, hi = (uint64_t)block_max_u32<NT>(km, red + 2 * (NT / 64)) + 1;
+        bool prefix = false;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (count_ge<NT, PER>(kr, (uint32_t)mid, red, parity) >= K) lo = mid;
+            const int c = count_ge<NT, PER>(kr, (uint32_t)mid, red, parity);
+            if (c >= kmin && c <= K && kmin >= 0) {  // uniform: c is a block total
+                lo = mid;
+                prefix = true;
+                break;
+            }
+            if (c >= K) lo = mid;
             else hi = mid;
         }
-        T = (uint32_t)lo;
-        const int greater = (hi >> 32) ? 0 : count_ge<NT, PER>(kr, (uint32_t)hi, red, parity);
-        need_eq = all_ties ? cap : K - greater;
+        if (prefix) {
+            T = (uint32_t)lo - 1u;  // keys > T are exactly the keys >= the probe; no partial ties
+            need_eq = 0;
+        } else {
+            T = (uint32_t)lo;
+            const int greater = (hi >> 32) ? 0 : count_ge<NT, PER>(kr, (uint32_t)hi, red, parity);
+            need_eq = all_ties ? cap : K - greater;
+        }
     }
     __syncthreads();
     // Compaction.  Callers sort the selected keys, so keys > T go out in any order: one scan of
@@ -873,7 +888,8 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 #define NMS_STAMP(acc) do { } while (0)
 #endif
     while (true) {
-        const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red);
+        // any prefix of the global order between 3M/4 and M candidates serves a round
+        const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red, false, 3 * M / 4);
         NMS_STAMP(t_sel);
         if (m == 0) break;
         for (int t = tid; t < NS; t += NT) S.hist[t] = 0;

@@ -9,7 +9,9 @@
 //   MEMSET         p0 ptr; i0 bytes
 //   PREPROCESS     p0 x[B,3,H,W]; p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
 //   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0; p6 w3 bf16 planes|0;
-//                  p7 in_shift|0; i24 in_relu;
+//                  p7 in_shift|0; i24 in_relu; p8 x3 scratch [3][B*H*W*Cin] bf16 | 0 (pre-split input
+//                  planes for the 256 x 128 bf16x6 tile: the split and the input transform run once
+//                  per input element instead of once per N tile)
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
@@ -84,6 +86,7 @@ static ConvParams conv_params(const edgedet_op& o) {
     p.w3 = P<const void>(o, 6);
     p.in_shift = P<const float>(o, 7);
     p.in_relu = (int)I[24];
+    p.x3 = P<void>(o, 8);
     p.B = (int)I[0];
     p.H = (int)I[1];
     p.W = (int)I[2];

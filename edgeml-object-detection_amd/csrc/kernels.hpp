@@ -16,6 +16,7 @@ struct ConvParams {
     const void* w3;         // bf16 split planes [3][Cout][Kpad] or null (bf16x6 tiles)
     const float* in_shift;  // [B][Cin] or null: input transform x * in_scale + in_shift (GroupNorm apply)
     int in_relu;            // ReLU on the transformed input (GroupNorm + ReLU, LastLevelP6P7's relu(P6))
+    void* x3;               // scratch for the pre-split input planes [3][B*H*W][Cin] bf16, or null
     int B, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, act;
     int K, Kpad, M;
     int x_pstride, y_pstride, res_pstride;

@@ -43,7 +43,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features")
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -82,6 +82,8 @@ def lib():
                                  _vp, _vp]
     L.edgedet_conv2d_ex.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
                                     _vp, _vp, _i32, _vp]
+    L.edgedet_conv2d_x3.argtypes = [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
+                                    _i32, _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
     L.edgedet_box_correct.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _dbl, _vp, _i64, _vp]
     L.edgedet_orie_ap.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _vp]
@@ -97,7 +99,7 @@ def lib():
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
                  "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features"):
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L
@@ -160,20 +162,26 @@ def split_bf16x3(w):
     return out
 
 
-def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, tile=0, in_scale=None, w3=None):
+def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, tile=0, in_scale=None, w3=None,
+                presplit=False):
     """Fused conv (+ folded BN) + residual + activation on NHWC; w_packed from plan.pack_conv_weight.
 
     tile=0 goes through the C entry point edgedet_conv2d_ex (automatic tile choice; with the split
     weight planes ``w3`` the compute-bound tiles run bf16x6); a non-zero tile (or an SE ``in_scale``
-    [B, Cin]) runs one CONV plan record so every kernel variant is testable.
+    [B, Cin]) runs one CONV plan record so every kernel variant is testable.  presplit=True hands the
+    kernel an x3 scratch (edgedet_conv2d_x3: tile 25 then splits the input once, up front).
     """
     _need_cuda(x, w_packed, bias, res, in_scale, w3)
     B, H, W, Cin = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
+    x3 = torch.empty(3 * B * H * W * Cin, dtype=torch.int16, device=x.device) if presplit else None
     if tile == 0 and in_scale is None:
-        if w3 is None:
+        if x3 is not None:
+            check(lib().edgedet_conv2d_x3(_ptr(x), _ptr(x3), B, H, W, Cin, _ptr(w_packed), _ptr(w3), _ptr(bias), cout,
+                                          k, k, stride, pad, ACT[act], _ptr(res), _ptr(y), 0, stream_handle()))
+        elif w3 is None:
             check(lib().edgedet_conv2d(_ptr(x), B, H, W, Cin, _ptr(w_packed), _ptr(bias), cout, k, k, stride, pad,
                                        ACT[act], _ptr(res), _ptr(y), stream_handle()))
         else:
@@ -187,7 +195,7 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     vals = [B, H, W, Cin, Ho, Wo, cout, k, k, stride, pad, ACT[act], K, kpad, Cin, cout, cout, H * W * Cin,
             Ho * Wo * cout, Ho * Wo * cout, 0, Ho, Wo, tile]
     rec[0]["i"][:len(vals)] = vals
-    for j, t in enumerate((x, w_packed, bias, y, res, in_scale, w3)):
+    for j, t in enumerate((x, w_packed, bias, y, res, in_scale, w3, None, x3)):
         rec[0]["p"][j] = 0 if t is None else t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
     return y

@@ -31,6 +31,9 @@ if CONV_MATH not in ("bf16x6", "f32"):
 # Measured tile per conv shape on gfx950 (tools/tune_conv.py); shapes not listed fall back to the
 # library's heuristic (csrc/conv.hip choose_tile).
 _TILES_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "conv_tiles_gfx950.json")
+# Pre-split conv inputs for the 256 x 128 bf16x6 tile (csrc/conv.hip split_act_kernel): one x3 scratch
+# per lane, sized for the largest input it serves.  EDGEDET_CONV_PRESPLIT=0 keeps the in-loop split.
+CONV_PRESPLIT = os.environ.get("EDGEDET_CONV_PRESPLIT", "1") == "1"
 CONV_TILES = {}
 if os.path.exists(_TILES_PATH) and os.environ.get("EDGEDET_CONV_TUNED", "1") == "1":
     import json as _json
@@ -214,6 +217,18 @@ class Plan:
         self.consts.append((b, a))
         return b
 
+    def x3_scratch(self, n):
+        """The current lane's pre-split scratch, grown to at least n uint16 (ops of one lane run in
+        order on one stream, so one scratch serves all of them)."""
+        lane = getattr(self, "_lane", 0)
+        d = self.__dict__.setdefault("_x3", {})
+        b = d.get(lane)
+        if b is None:
+            b = d[lane] = self.buf((n,), torch.int16, name=f"x3.lane{lane}")
+        elif b.shape[0] < n:
+            b.shape, b.nbytes = (n,), 2 * n
+        return b
+
     def add(self, op):
         if op.lane == 0 and getattr(self, "_lane", 0):
             op.lane = self._lane
@@ -333,4 +348,10 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
         t = CONV_TILES.get(conv_key(op))
         if t and (w3 is not None or t < 20):
             op.i[23] = int(t)
+    # only where an input transform is fused: the split pass then also takes the per-element GN / SE
+    # arithmetic out of the GEMM loop (measured: GN+ReLU head conv 1.83 -> 1.74 ms); for a plain input
+    # the extra pass costs more than the in-loop split (box head 2.48 -> 2.60 ms)
+    xf = in_scale is not None or in_shift is not None or in_relu
+    if CONV_PRESPLIT and xf and w3 is not None and C % 32 == 0 and op.i[23] in (0, 25):
+        op.p[8] = plan.x3_scratch(3 * B * H * W * C)
     return plan.add(op)

@@ -131,6 +131,16 @@ int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t C
                       const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH, int32_t KW,
                       int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
                       void* stream);
+/*
+ * edgedet_conv2d_ex with a caller-owned scratch x3 of 3 * B*H*W*Cin uint16: when the 256 x 128
+ * bf16x6 tile runs (tile 25, Cin % 32 == 0) the input is split into three bf16 planes once, by a
+ * separate pass into x3, instead of inside every N tile of the GEMM.  Results are bit-identical to
+ * edgedet_conv2d_ex; x3 may be null (then this is edgedet_conv2d_ex).
+ */
+int edgedet_conv2d_x3(const float* x, uint16_t* x3, int64_t B, int64_t H, int64_t W, int64_t Cin,
+                      const float* w, const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH,
+                      int32_t KW, int32_t stride, int32_t pad, int32_t act, const float* res, float* y,
+                      int32_t tile, void* stream);
 /* w [n] fp32 -> out [3][n] bf16 bit patterns: x0 = RN(x), x1 = RN(x - x0), x2 = x - x0 - x1 (exact). */
 int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream);
 

@@ -224,6 +224,35 @@ def test_conv_bf16x6_matches_torch(case, tile):
     _conv_case(*case, tile=tile, x6=True)
 
 
+@pytest.mark.parametrize("se", [False, True])
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (2, 3, 4, 7)] + [(2, 7, 7, 256, 200, 3, 1, "RE", False)])
+def test_conv_bf16x6_presplit_bit_identical(case, se):
+    """Tile 25 with the input split up front (split_act_kernel into the x3 scratch, SE scale applied
+    there) equals the in-loop split bit for bit, and both match torch."""
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight
+    B, H, W, Cin, Cout, k, s, act, res = case
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, H, W, Cin, generator=g).to(DEV)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = (torch.randn(Cout, generator=g) * 0.1).to(DEV)
+    sc = torch.rand(B, Cin, generator=g).to(DEV) if se else None
+    Ho, Wo = (H + 2 * ((k - 1) // 2) - k) // s + 1, (W + 2 * ((k - 1) // 2) - k) // s + 1
+    r = torch.randn(B, Ho, Wo, Cout, generator=g).to(DEV) if res else None
+    wp = torch.from_numpy(pack_conv_weight(w.numpy())[0]).to(DEV)
+    w3 = ops.split_bf16x3(wp)
+    outs = [ops.conv2d_nhwc(x, wp, b, Cout, k, s, (k - 1) // 2, act, r, tile=25, in_scale=sc, w3=w3, presplit=ps)
+            for ps in (False, True)]
+    assert torch.equal(outs[0], outs[1])
+    xin = x.permute(0, 3, 1, 2).cpu() * (sc.cpu()[:, :, None, None] if se else 1)
+    ref = F.conv2d(xin, w, b.cpu(), s, (k - 1) // 2)
+    if res:
+        ref = ref + r.permute(0, 3, 1, 2).cpu()
+    ref = _act(ref, act)
+    err = (outs[1].permute(0, 3, 1, 2).cpu() - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
 @pytest.mark.parametrize("tile", [22, 23, 24, 25])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)

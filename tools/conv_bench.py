@@ -45,9 +45,11 @@ def main():
         Wo = (W + 2 * pad - k) // s + 1
         flops = 2.0 * B * Ho * Wo * Cout * k * k * Cin
         res = []
-        for t in (int(v) for v in a.tiles.split(",")):
+        for tv in a.tiles.split(","):  # "25p": tile 25 with the input pre-split (x3 scratch)
+            t, ps = int(tv.rstrip("p")), tv.endswith("p")
             for use3 in ((False, True) if t == 0 else (t >= 20,)):
-                f = lambda: ops.conv2d_nhwc(x, wp, b, Cout, k, s, pad, "RE", tile=t, w3=w3 if use3 else None)
+                f = lambda: ops.conv2d_nhwc(x, wp, b, Cout, k, s, pad, "RE", tile=t, w3=w3 if use3 else None,
+                                            presplit=ps)
                 f()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,7 +59,7 @@ def main():
                 e1.record()
                 e1.synchronize()
                 ms = e0.elapsed_time(e1) / a.reps
-                res.append(f"tile{t}{'x6' if use3 and t == 0 else ''}: {ms:.3f} ms {flops / ms / 1e9:.1f} TF")
+                res.append(f"tile{tv}{'x6' if use3 and t == 0 else ''}: {ms:.3f} ms {flops / ms / 1e9:.1f} TF")
         print(f"{name:14s} M={B * Ho * Wo} N={Cout} K={k * k * Cin}: " + " | ".join(res), flush=True)
 
 
