@@ -353,9 +353,10 @@ __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, int* red) {
 // caller that consumes candidates in global order, round by round, needs.
 template <int NT, int PER>
 __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsigned long long* keys, int* wsum,
-                                int* red, bool all_ties = false, int kmin = -1) {
+                                int* red, bool all_ties = false, int kmin = -1, int* nvalid_out = nullptr) {
     int parity = 0;
     const int nvalid = count_ge<NT, PER>(kr, 1u, red, parity);
+    if (nvalid_out) *nvalid_out = nvalid;
     uint32_t T = 1u;
     int need_eq = 0;
     const bool take_all = nvalid <= K;
@@ -889,7 +890,8 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 #endif
     while (true) {
         // any prefix of the global order between 3M/4 and M candidates serves a round
-        const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red, false, 3 * M / 4);
+        int nleft;
+        const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red, false, 3 * M / 4, &nleft);
         NMS_STAMP(t_sel);
         if (m == 0) break;
         for (int t = tid; t < NS; t += NT) S.hist[t] = 0;
@@ -1094,7 +1096,7 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 #ifdef NMS_PROFILE
         ++rounds;
 #endif
-        if (total >= N || m < M) break;
+        if (total >= N || m >= nleft) break;  // a round may be a prefix shorter than M
     }
     if (tid == 0) out_count[b] = total < N ? total : N;
 #ifdef NMS_PROFILE
