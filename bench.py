@@ -115,6 +115,10 @@ def op_work(op):
         return "conv", flops, byts
     if k == O.DWCONV:
         B, H, W, C, Ho, Wo, K = (i[j] for j in range(7))
+        if op.p.get(5) is not None:  # fused MBConv front: 1x1 expansion of the Cin-wide input + depthwise
+            cin = i[11]
+            return ("mbconv", 2.0 * B * (H * W * C * cin + Ho * Wo * C * K * K),
+                    4.0 * (B * H * W * cin + B * Ho * Wo * C + C * (cin + K * K)))
         return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
     if k == O.PREPROCESS:
         B, H, W, Ho, Wo, Hp, Wp = (i[j] for j in range(7))

@@ -16,6 +16,8 @@
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
+//                  fused MBConv front when p5 != 0: p0 is the block input [B,H,W,i11 Cin], p5 the
+//                  1x1 expansion weight [C][i12 ld], p6 its bias, i13 its activation
 //                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16)
 //   CHANNEL_MEAN   p0 x[B,HW,C]; p1 mean[B,C]; i0..2 B,HW,C
 //   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; p6 hidden[B,S];
@@ -160,6 +162,11 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.pad = (int)I[8];
             p.act = (int)I[9];
             p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
+            p.w1 = P<const float>(o, 5);
+            p.b1 = P<const float>(o, 6);
+            p.Cin = (int)I[11];
+            p.w1_ld = (int)I[12];
+            p.act1 = (int)I[13];
             return dwconv_launch(p, s);
         }
         case EDGEDET_OP_CHANNEL_MEAN:

@@ -279,7 +279,173 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------ fused MBConv front
+// expand 1x1 (+BN, act1) -> depthwise KxK stride S (+BN, act2) for an InvertedResidual without SE
+// (torchvision mobilenetv3 InvertedResidual): the 6x-wide expanded tensor lives
+// only in LDS.  Block = one image, an 8 x 8 output tile and CC = 32 expanded channels (4 waves):
+//   1. the input halo tile ((8-1)*S + K)^2 x Cin is loaded into LDS (zeros outside the image), rows
+//      padded to Cin + 1 floats so the MFMA operand reads are conflict-free;
+//   2. expansion on the matrix cores: [halo pixels, padded to 32-row tiles] x [Cin] x [32 channels]
+//      with v_mfma_f32_32x32x2_f32 (exact fp32 products), + bias, act1; pixels outside the image are
+//      zero (the depthwise conv pads the expanded tensor);
+//   3. depthwise: thread (output pixel, channel quad), taps in (kh, kw) order as dw_group, + bias, act2.
+// Measured slower than the unfused pair on every SSDLite shape (tools/mb_bench.py, B=16: block 0.2
+// 69 vs 75 us, 0.7 61 vs 33 us): each block is three dependent latency phases (halo load, MFMA
+// expansion, depthwise) at two blocks per CU (70-100 KiB of LDS), and the halo load alone costs
+// half of the unfused pair.  So the lowering keeps the pair (EDGEDET_MBCONV_FUSE=1 selects this).
+constexpr int MB_TILE = 8, MB_CC = 32, MB_ES = MB_CC + 4;
+typedef float mb_floatx16 __attribute__((ext_vector_type(16)));
+
+template <int K, int S>
+struct MbGeom {
+    static constexpr int IH = (MB_TILE - 1) * S + K, IP = IH * IH, IPP = (IP + 31) / 32 * 32;
+    static size_t lds_bytes(int cin) {
+        return sizeof(float) * ((size_t)IPP * (cin + 4) + (size_t)MB_CC * (cin + 4) + (size_t)IPP * MB_ES);
+    }
+};
+
+template <int K, int S, int ACT1>
+__global__ void __launch_bounds__(256) mbconv_front_kernel(DwParams p, int tiles_w, int nchunk) {
+    using G = MbGeom<K, S>;
+    constexpr int IH = G::IH, IP = G::IP, IPP = G::IPP;
+    extern __shared__ __attribute__((aligned(16))) float mb_sm[];
+    const int Cin = p.Cin, XS = Cin + 4;
+    float* xs = mb_sm;            // [IPP][Cin + 4]: 16-B rows, 16 consecutive rows on distinct banks
+    float* ws = xs + IPP * XS;    // [MB_CC][Cin + 4]
+    float* es = ws + MB_CC * XS;  // [IPP][MB_ES]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int b = blockIdx.y;
+    const int chunk = blockIdx.x % nchunk, tile = blockIdx.x / nchunk;
+    const int oh0 = (tile / tiles_w) * MB_TILE, ow0 = (tile % tiles_w) * MB_TILE;
+    const int c0 = chunk * MB_CC;
+    const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
+
+    // 1. input halo and the chunk's expansion weights
+    const int q4 = Cin >> 2;
+    const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
+    for (int v = tid; v < IPP * q4; v += 256) {
+        const int pp = v / q4, q = v - pp * q4;
+        const int ih = ih0 + pp / IH, iw = iw0 + pp % IH;
+        f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (pp < IP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+            xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * Cin + 4 * q);
+        *reinterpret_cast<f32x4*>(xs + pp * XS + 4 * q) = xv;
+    }
+    for (int v = tid; v < MB_CC * q4; v += 256) {
+        const int n = v / q4, q = v - n * q4;
+        f32x4 wv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (c0 + n < p.C) wv = *reinterpret_cast<const f32x4*>(p.w1 + (int64_t)(c0 + n) * p.w1_ld + 4 * q);
+        *reinterpret_cast<f32x4*>(ws + n * XS + 4 * q) = wv;
+    }
+    __syncthreads();
+
+    // 2. expansion: wave w takes 32-pixel row tiles w, w + 4, ...; lane half h supplies the channels
+    //    [h * Cin/2, (h+1) * Cin/2) in order, four MFMA steps per ds_read_b128 of each operand
+    {
+        const int l32 = lane & 31, h = lane >> 5;
+        const int n = l32, c = c0 + n;
+        const int kh = Cin >> 1;  // Cin % 8 == 0
+        const float bias1 = c < p.C ? p.b1[c] : 0.f;
+        const float* br = ws + n * XS + h * kh;
+        for (int t = wid; t < IPP / 32; t += 4) {
+            mb_floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+            const float* ar = xs + (32 * t + l32) * XS + h * kh;
+            for (int k = 0; k < kh; k += 4) {
+                const f32x4 av = *reinterpret_cast<const f32x4*>(ar + k);
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(br + k);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int ih = ih0 + m / IH, iw = iw0 + m % IH;
+                const bool in = m < IP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && c < p.C;
+                es[m * MB_ES + n] = in ? apply_act(acc[r] + bias1, ACT1) : 0.f;  // ACT1 constant: no branch
+            }
+        }
+    }
+    __syncthreads();
+
+    // 3. depthwise: 64 pixels x 8 channel quads, two per thread
+    for (int it = tid; it < MB_TILE * MB_TILE * (MB_CC / 4); it += 256) {
+        const int o = it >> 3, q = it & 7;
+        const int oh = oh0 + o / MB_TILE, ow = ow0 + o % MB_TILE;
+        const int c = c0 + 4 * q;
+        if (oh >= p.Ho || ow >= p.Wo || c >= p.C) continue;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int lh0 = (o / MB_TILE) * S, lw0 = (o % MB_TILE) * S;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+            if ((unsigned)(ih0 + lh0 + kh) >= (unsigned)p.H) continue;  // dw_group skips rows outside the map
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const f32x4 xv = *reinterpret_cast<const f32x4*>(es + ((lh0 + kh) * IH + lw0 + kw) * MB_ES + 4 * q);
+                const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * K + kw) * p.C + c);
+                acc.x = fmaf(xv.x, wv.x, acc.x);
+                acc.y = fmaf(xv.y, wv.y, acc.y);
+                acc.z = fmaf(xv.z, wv.z, acc.z);
+                acc.w = fmaf(xv.w, wv.w, acc.w);
+            }
+        }
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
+        f32x4 v;
+        v.x = apply_act(acc.x + bv.x, p.act);
+        v.y = apply_act(acc.y + bv.y, p.act);
+        v.z = apply_act(acc.z + bv.z, p.act);
+        v.w = apply_act(acc.w + bv.w, p.act);
+        *reinterpret_cast<f32x4*>(p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow) * p.C + c) = v;
+    }
+}
+
+template <int K, int S>
+static int mbconv_front_launch(const DwParams& p, hipStream_t s) {
+    const size_t lds = MbGeom<K, S>::lds_bytes(p.Cin);
+    EDGEDET_REQUIRE(lds <= 160 * 1024, "mbconv_front: input halo tile too large for LDS");
+    const int tiles_w = cdiv(p.Wo, MB_TILE), tiles = cdiv(p.Ho, MB_TILE) * tiles_w, nchunk = cdiv(p.C, MB_CC);
+    EDGEDET_REQUIRE(p.act1 >= 0 && p.act1 <= 3, "mbconv_front: expansion activation none / RE / R6 / HS");
+    static bool attr = false;
+    auto k = p.act1 == 0 ? mbconv_front_kernel<K, S, 0>
+                         : p.act1 == 1 ? mbconv_front_kernel<K, S, 1>
+                                       : p.act1 == 2 ? mbconv_front_kernel<K, S, 2> : mbconv_front_kernel<K, S, 3>;
+    if (!attr) {
+        for (auto f : {mbconv_front_kernel<K, S, 0>, mbconv_front_kernel<K, S, 1>, mbconv_front_kernel<K, S, 2>,
+                       mbconv_front_kernel<K, S, 3>})
+            EDGEDET_CHECK_HIP(
+                hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3((unsigned)(tiles * nchunk), (unsigned)p.B), dim3(256), lds, s, p, tiles_w, nchunk);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+// LDS bytes the fused front needs (0 = shape not supported); the plan uses it to decide fusion.
+extern "C" int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin) {
+    if (K == 3 && stride == 1) return (int64_t)MbGeom<3, 1>::lds_bytes(Cin);
+    if (K == 3 && stride == 2) return (int64_t)MbGeom<3, 2>::lds_bytes(Cin);
+    if (K == 5 && stride == 1) return (int64_t)MbGeom<5, 1>::lds_bytes(Cin);
+    if (K == 5 && stride == 2) return (int64_t)MbGeom<5, 2>::lds_bytes(Cin);
+    return 0;
+}
+
 int dwconv_launch(const DwParams& p, hipStream_t s) {
+    if (p.w1) {
+        EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y && p.b1, "mbconv_front: null pointer");
+        EDGEDET_REQUIRE(!p.part, "mbconv_front: no SE squeeze");
+        EDGEDET_REQUIRE(p.C % 8 == 0 && p.Cin % 8 == 0 && p.w1_ld % 4 == 0 && p.w1_ld >= p.Cin,
+                        "mbconv_front: C % 8, Cin % 8 and the weight row stride");
+        EDGEDET_REQUIRE(p.pad == (p.K - 1) / 2, "mbconv_front: 'same' padding only");
+        if (p.K == 3 && p.stride == 1) return mbconv_front_launch<3, 1>(p, s);
+        if (p.K == 3 && p.stride == 2) return mbconv_front_launch<3, 2>(p, s);
+        if (p.K == 5 && p.stride == 1) return mbconv_front_launch<5, 1>(p, s);
+        if (p.K == 5 && p.stride == 2) return mbconv_front_launch<5, 2>(p, s);
+        EDGEDET_REQUIRE(false, "mbconv_front: K in {3, 5}, stride in {1, 2}");
+    }
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
     if (p.part) EDGEDET_REQUIRE(p.parts >= 1 && p.parts <= SE_PARTS, "dwconv: 1..16 SE partial sums");
@@ -748,6 +914,32 @@ extern "C" int edgedet_roi_align(const float* feat, int64_t B, int64_t H, int64_
     p.sr = sampling_ratio;
     p.out = out;
     return roi_align_launch(p, (hipStream_t)stream);
+}
+
+extern "C" int edgedet_mbconv_front(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w1,
+                                    int64_t w1_ld, const float* b1, int32_t act1, int64_t C, const float* w,
+                                    const float* bias, int32_t K, int32_t stride, int32_t act, float* y, void* stream) {
+    DwParams p{};
+    p.x = x;
+    p.w1 = w1;
+    p.b1 = b1;
+    p.Cin = (int)Cin;
+    p.w1_ld = (int)w1_ld;
+    p.act1 = act1;
+    p.w = w;
+    p.bias = bias;
+    p.y = y;
+    p.B = (int)B;
+    p.H = (int)H;
+    p.W = (int)W;
+    p.C = (int)C;
+    p.K = K;
+    p.stride = stride;
+    p.pad = (K - 1) / 2;
+    p.act = act;
+    p.Ho = (int)((H + 2 * p.pad - K) / stride + 1);
+    p.Wo = (int)((W + 2 * p.pad - K) / stride + 1);
+    return dwconv_launch(p, (hipStream_t)stream);
 }
 
 extern "C" int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,

@@ -20,6 +20,11 @@ from . import arch
 from . import ops
 from .plan import BufView, Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_weight, pack_dw_weight, split_bf16x3
 
+# InvertedResidual expand + depthwise as one fused kernel (no SE in between), with the expanded
+# tensor kept in LDS.  Off by default: measured slower than the two ops (csrc/layers.hip
+# mbconv_front_kernel header); EDGEDET_MBCONV_FUSE=1 selects it.
+MBCONV_FUSE = os.environ.get("EDGEDET_MBCONV_FUSE", "0") == "1"
+
 
 def _np(t):
     return t.detach().cpu().to(torch.float64).numpy()
@@ -286,10 +291,34 @@ class SSDLite320(_Detector):
                      {0: part, 1: w1, 2: b1, 3: w2t, 4: b2, 5: scale, 6: hidden}, name=p))
             return scale
 
+        def mbfront(cur, pe, pd, k, stride, act):
+            """Expand 1x1 + depthwise as one fused op (csrc/layers.hip mbconv_front_kernel), or None
+            when the shapes do not fit it."""
+            xb, xs = cur
+            w1, b1, _, kpad1, cin = self._conv_bn(pe + ".0.weight", pe + ".1", self.BN_EPS)
+            w, b, _, _, c = self._conv_bn(pd + ".0.weight", pd + ".1", self.BN_EPS)
+            ipp = ((7 * stride + k) ** 2 + 31) // 32 * 32  # LDS of the kernel (csrc/layers.hip MbGeom)
+            lds = 4 * (ipp * (cin + 4) + 32 * (cin + 4) + ipp * 36)
+            if not (MBCONV_FUSE and xs[3] == cin and cin % 8 == 0 and c % 8 == 0 and lds <= 160 * 1024):
+                return None
+            pad = (k - 1) // 2
+            Ho = (xs[1] + 2 * pad - k) // stride + 1
+            Wo = (xs[2] + 2 * pad - k) // stride + 1
+            ys = (B, Ho, Wo, c)
+            y = P.buf(ys, name=pd + sfx)
+            P.add(Op(ops.DWCONV, {0: B, 1: xs[1], 2: xs[2], 3: c, 4: Ho, 5: Wo, 6: k, 7: stride, 8: pad,
+                                  9: ops.ACT[act], 10: 0, 11: cin, 12: kpad1, 13: ops.ACT[act]},
+                     {0: xb, 1: w, 2: b, 3: y, 4: None, 5: w1, 6: b1}, name=pe + "+" + pd.rsplit(".", 1)[-1]))
+            return (y, ys)
+
         def inverted_residual(cur, cnf, base):
             cin, k, exp, cout, use_se, act, stride = cnf
             pe, pd, ps, pp = arch.block_prefixes(cnf, base)
             y = cur
+            fused = mbfront(y, pe, pd, k, stride, act) if pe and not use_se and not pack_only else None
+            if fused is not None:
+                res = cur[0] if (stride == 1 and cin == cout) else None
+                return conv(fused, pp, 1, 1, None, res=res)
             if pe:
                 y = conv(y, pe, 1, 1, act)
             y = dw(y, pd, k, stride, act, se_part=use_se)

@@ -43,7 +43,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3")
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -85,6 +85,10 @@ def lib():
     L.edgedet_conv2d_x3.argtypes = [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
                                     _i32, _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
+    L.edgedet_mbconv_front_lds.argtypes = [_i32, _i32, _i64]
+    L.edgedet_mbconv_front_lds.restype = ctypes.c_int64
+    L.edgedet_mbconv_front.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32, _i32,
+                                       _i32, _vp, _vp]
     L.edgedet_box_correct.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _dbl, _vp, _i64, _vp]
     L.edgedet_orie_ap.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _vp]
     L.edgedet_map_eval.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]
@@ -99,7 +103,7 @@ def lib():
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
                  "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3"):
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L
@@ -198,6 +202,22 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     for j, t in enumerate((x, w_packed, bias, y, res, in_scale, w3, None, x3)):
         rec[0]["p"][j] = 0 if t is None else t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
+    return y
+
+
+def mbconv_front_nhwc(x, w1_packed, b1, act1, w_taps, bias, k, stride, act):
+    """Fused InvertedResidual front: 1x1 expansion (w1_packed [C][ld] from plan.pack_conv_weight,
+    folded BN, act1) then depthwise k x k / stride (w_taps from plan.pack_dw_weight, act), the
+    expanded tensor kept in LDS (csrc/layers.hip mbconv_front_kernel)."""
+    _need_cuda(x, w1_packed, b1, w_taps, bias)
+    B, H, W, Cin = x.shape
+    C, ld = w1_packed.shape
+    pad = (k - 1) // 2
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, Ho, Wo, C), dtype=torch.float32, device=x.device)
+    check(lib().edgedet_mbconv_front(_ptr(x), B, H, W, Cin, _ptr(w1_packed), ld, _ptr(b1), ACT[act1], C, _ptr(w_taps),
+                                     _ptr(bias), k, stride, ACT[act], _ptr(y), stream_handle()))
     return y
 
 
