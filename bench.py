@@ -120,6 +120,9 @@ def op_work(op):
             return ("mbconv", 2.0 * B * (H * W * C * cin + Ho * Wo * C * K * K),
                     4.0 * (B * H * W * cin + B * Ho * Wo * C + C * (cin + K * K)))
         return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
+    if k == O.SSD_STEM:  # stem conv 3x3 s2 (4 -> 16) + depthwise 3x3 + projection 16 -> 16 + residual
+        B, H, W, Ho, Wo = (i[j] for j in range(5))
+        return "stem", 2.0 * B * Ho * Wo * 16 * (36 + 9 + 16), 4.0 * (B * H * W * 4 + B * Ho * Wo * 16)
     if k == O.PREPROCESS:
         B, H, W, Ho, Wo, Hp, Wp = (i[j] for j in range(7))
         return "preprocess", 0.0, 4.0 * (B * 3 * H * W + B * Hp * Wp * 4)

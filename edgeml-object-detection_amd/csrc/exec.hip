@@ -15,6 +15,8 @@
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto)
+//   SSD_STEM       p0 x NHWC4; p1 w0 [16][i5]; p2 b0; p3 wd [9][16]; p4 bd; p5 w1 [16][i6]; p6 b1; p7 y;
+//                  i0..4 B,H,W,Ho,Wo (SSDLite features.0.0 + features.0.1 fused)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
 //                  fused MBConv front when p5 != 0: p0 is the block input [B,H,W,i11 Cin], p5 the
 //                  1x1 expansion weight [C][i12 ld], p6 its bias, i13 its activation
@@ -303,6 +305,25 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.chunk = (int)I[16];
             p.nchunk = (int)I[17];
             return retina_select_launch(p, seg_out(o, 3, (int)I[5]), s);
+        }
+        case EDGEDET_OP_SSD_STEM: {
+            StemParams p{};
+            p.x = P<const float>(o, 0);
+            p.w0 = P<const float>(o, 1);
+            p.b0 = P<const float>(o, 2);
+            p.wd = P<const float>(o, 3);
+            p.bd = P<const float>(o, 4);
+            p.w1 = P<const float>(o, 5);
+            p.b1 = P<const float>(o, 6);
+            p.y = P<float>(o, 7);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.Ho = (int)I[3];
+            p.Wo = (int)I[4];
+            p.ld0 = (int)I[5];
+            p.ld1 = (int)I[6];
+            return ssd_stem_launch(p, s);
         }
         case EDGEDET_OP_RETINA_CLASS_NMS: {
             RetinaNmsParams p{};

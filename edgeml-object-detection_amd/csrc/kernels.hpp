@@ -169,6 +169,20 @@ int conv_resolve_tile(const ConvParams& p, int tile);
 int conv_launch(ConvParams p, int tile, hipStream_t s);
 int preprocess_launch(const PreParams& p, hipStream_t s);
 int dwconv_launch(const DwParams& p, hipStream_t s);
+
+// SSDLite stem + features.0.1 in one pass (csrc/layers.hip ssd_stem_kernel).
+struct StemParams {
+    const float* x;   // [B][H][W][4] preprocessed NHWC4 image
+    const float* w0;  // stem conv [16][ld0] (3x3, Cin 4, folded BN), b0 [16], hardswish
+    const float* b0;
+    const float* wd;  // features.0.1 depthwise [9][16], bd [16], ReLU
+    const float* bd;
+    const float* w1;  // features.0.1 projection [16][ld1], b1 [16], + residual (the stem output)
+    const float* b1;
+    float* y;         // [B][Ho][Wo][16]
+    int B, H, W, Ho, Wo, ld0, ld1;
+};
+int ssd_stem_launch(const StemParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);
 int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
                  float* hidden, float* scale, int B, int C, int S, int HW, int parts, hipStream_t s);

@@ -279,6 +279,124 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------ SSDLite stem
+// features.0.0 (conv 3x3 s2, 3(+1 pad) -> 16, folded BN, hardswish) and features.0.1 (depthwise 3x3
+// 16 + BN + ReLU, projection 1x1 16 -> 16 + BN, + the stem output) in one pass: the two 16-channel
+// 160x160 tensors between them never reach HBM.  Block = one image, a 16 x 16 output tile:
+//   1. the 37 x 37 x 4 input tile (stride-2 receptive field of the 18 x 18 stem halo) into LDS;
+//   2. stem outputs on the 18 x 18 halo (zero outside the map: the depthwise pads them), one pixel x
+//      16 channels per thread, taps in the packed (kh, kw, ci) order;
+//   3. per output pixel: depthwise (taps (kh, kw) as dw_group), projection, + bias, + residual.
+// The weights are wave-uniform scalar loads.
+constexpr int STEM_T = 16, STEM_SH = STEM_T + 2, STEM_XH = 2 * STEM_SH + 1, STEM_SS = 20;
+
+__global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
+    __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
+    __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
+    const int tid = threadIdx.x, b = blockIdx.y;
+    const int oh0 = (blockIdx.x / tiles_w) * STEM_T, ow0 = (blockIdx.x % tiles_w) * STEM_T;
+    const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
+    const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
+    const float* xb = p.x + (int64_t)b * p.H * p.W * 4;
+    for (int v = tid; v < STEM_XH * STEM_XH; v += 256) {
+        const int ih = xh0 + v / STEM_XH, iw = xw0 + v % STEM_XH;
+        f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+            xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * 4);
+        *reinterpret_cast<f32x4*>(xs + 4 * v) = xv;
+    }
+    __syncthreads();
+    for (int v = tid; v < STEM_SH * STEM_SH; v += 256) {
+        const int lh = v / STEM_SH, lw = v % STEM_SH;
+        const bool in = (unsigned)(sh0 + lh) < (unsigned)p.Ho && (unsigned)(sw0 + lw) < (unsigned)p.Wo;
+        f32x4 xt[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            xt[t] = *reinterpret_cast<const f32x4*>(xs + 4 * ((2 * lh + t / 3) * STEM_XH + 2 * lw + t % 3));
+        float* d = ss + v * STEM_SS;
+#pragma unroll
+        for (int co = 0; co < 16; ++co) {
+            const float* w = p.w0 + co * p.ld0;
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                acc = fmaf(w[4 * t + 0], xt[t].x, acc);
+                acc = fmaf(w[4 * t + 1], xt[t].y, acc);
+                acc = fmaf(w[4 * t + 2], xt[t].z, acc);
+                acc = fmaf(w[4 * t + 3], xt[t].w, acc);
+            }
+            d[co] = in ? apply_act(acc + p.b0[co], ACT_HSWISH) : 0.f;
+        }
+    }
+    __syncthreads();
+    const int lh = tid / STEM_T, lw = tid % STEM_T;
+    const int oh = oh0 + lh, ow = ow0 + lw;
+    if (oh >= p.Ho || ow >= p.Wo) return;
+    float dv[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dv[c] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+        if ((unsigned)(oh - 1 + kh) >= (unsigned)p.Ho) continue;  // dw_group skips rows outside the map
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const float* sv = ss + ((lh + kh) * STEM_SH + lw + kw) * STEM_SS;
+            const float* wv = p.wd + (kh * 3 + kw) * 16;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) dv[c] = fmaf(sv[c], wv[c], dv[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dv[c] = apply_act(dv[c] + p.bd[c], ACT_RELU);
+    const float* res = ss + ((lh + 1) * STEM_SH + lw + 1) * STEM_SS;
+    float out[16];
+#pragma unroll
+    for (int co = 0; co < 16; ++co) {
+        const float* w = p.w1 + co * p.ld1;
+        float acc = 0.f;
+#pragma unroll
+        for (int ci = 0; ci < 16; ++ci) acc = fmaf(w[ci], dv[ci], acc);
+        out[co] = (acc + p.b1[co]) + res[co];
+    }
+    float* yp = p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(yp + 4 * q) = f32x4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+}
+
+int ssd_stem_launch(const StemParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.w0 && p.b0 && p.wd && p.bd && p.w1 && p.b1 && p.y, "ssd_stem: null pointer");
+    EDGEDET_REQUIRE(p.Ho == (p.H - 1) / 2 + 1 && p.Wo == (p.W - 1) / 2 + 1, "ssd_stem: 3x3 stride 2 pad 1 shape");
+    EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
+    const int tiles_w = cdiv(p.Wo, STEM_T);
+    hipLaunchKernelGGL(ssd_stem_kernel, dim3((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B), dim3(256), 0, s,
+                       p, tiles_w);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W, const float* w0, int64_t ld0,
+                                const float* b0, const float* wd, const float* bd, const float* w1, int64_t ld1,
+                                const float* b1, float* y, void* stream) {
+    StemParams p{};
+    p.x = x;
+    p.w0 = w0;
+    p.b0 = b0;
+    p.wd = wd;
+    p.bd = bd;
+    p.w1 = w1;
+    p.b1 = b1;
+    p.y = y;
+    p.B = (int)B;
+    p.H = (int)H;
+    p.W = (int)W;
+    p.Ho = (int)((H - 1) / 2 + 1);
+    p.Wo = (int)((W - 1) / 2 + 1);
+    p.ld0 = (int)ld0;
+    p.ld1 = (int)ld1;
+    return ssd_stem_launch(p, (hipStream_t)stream);
+}
+
 // ------------------------------------------------------------------------------ fused MBConv front
 // expand 1x1 (+BN, act1) -> depthwise KxK stride S (+BN, act2) for an InvertedResidual without SE
 // (torchvision mobilenetv3 InvertedResidual): the 6x-wide expanded tensor lives

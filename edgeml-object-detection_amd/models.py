@@ -24,6 +24,9 @@ from .plan import BufView, Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_wei
 # tensor kept in LDS.  Off by default: measured slower than the two ops (csrc/layers.hip
 # mbconv_front_kernel header); EDGEDET_MBCONV_FUSE=1 selects it.
 MBCONV_FUSE = os.environ.get("EDGEDET_MBCONV_FUSE", "0") == "1"
+# SSDLite features.0.0 + features.0.1 as one kernel (csrc/layers.hip ssd_stem_kernel); =0 lowers the
+# three separate ops.
+SSD_STEM_FUSE = os.environ.get("EDGEDET_SSD_STEM_FUSE", "1") == "1"
 
 
 def _np(t):
@@ -327,8 +330,23 @@ class SSDLite320(_Detector):
             return conv(y[:2], pp, 1, 1, None, res=res, in_scale=scale)
 
         cfg = arch.mnv3_blocks(self.reduced_tail)
-        cur = conv(cur, "backbone.features.0.0", 3, 2, "HS", cin_pad=4)
-        for i in range(12):
+        first = 0
+        if SSD_STEM_FUSE and not pack_only and cfg[0] == (16, 3, 16, 16, False, "RE", 1):
+            # features.0.0 + features.0.1 as one op (csrc/layers.hip ssd_stem_kernel)
+            w0, b0, _, kpad0, _ = self._conv_bn("backbone.features.0.0.0.weight", "backbone.features.0.0.1",
+                                                self.BN_EPS, 4)
+            _, pd, _, pp = arch.block_prefixes(cfg[0], "backbone.features.0.1.block")
+            wd, bd, _, _, _ = self._conv_bn(pd + ".0.weight", pd + ".1", self.BN_EPS)
+            w1, b1, _, kpad1, _ = self._conv_bn(pp + ".0.weight", pp + ".1", self.BN_EPS)
+            Ho, Wo = (S - 1) // 2 + 1, (S - 1) // 2 + 1
+            ys = (B, Ho, Wo, 16)
+            y = P.buf(ys, name="backbone.features.0.1" + sfx)
+            P.add(Op(ops.SSD_STEM, {0: B, 1: S, 2: S, 3: Ho, 4: Wo, 5: kpad0, 6: kpad1},
+                     {0: x, 1: w0, 2: b0, 3: wd, 4: bd, 5: w1, 6: b1, 7: y}, name="backbone.features.0.0+0.1"))
+            cur, first = (y, ys), 1
+        else:
+            cur = conv(cur, "backbone.features.0.0", 3, 2, "HS", cin_pad=4)
+        for i in range(first, 12):
             cur = inverted_residual(cur, cfg[i], f"backbone.features.0.{i + 1}.block")
         _, k, exp, cout, _, act, stride = cfg[12]
         cur = conv(cur, "backbone.features.0.13", 1, 1, act)

@@ -21,6 +21,7 @@ MEMSET, PREPROCESS, CONV, DWCONV, CHANNEL_MEAN, SE_FC, MAXPOOL = 1, 2, 3, 4, 5, 
 SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX_CLASS_NMS = 8, 9, 10, 11, 12, 13, 14
 FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
 GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
+SSD_STEM = 21
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
@@ -43,7 +44,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds")
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds", "edgedet_ssd_stem")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -86,6 +87,7 @@ def lib():
                                     _i32, _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
     L.edgedet_mbconv_front_lds.argtypes = [_i32, _i32, _i64]
+    L.edgedet_ssd_stem.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]
     L.edgedet_mbconv_front_lds.restype = ctypes.c_int64
     L.edgedet_mbconv_front.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32, _i32,
                                        _i32, _vp, _vp]
@@ -103,7 +105,7 @@ def lib():
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
                  "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front"):
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_ssd_stem"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L
@@ -202,6 +204,17 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     for j, t in enumerate((x, w_packed, bias, y, res, in_scale, w3, None, x3)):
         rec[0]["p"][j] = 0 if t is None else t.data_ptr()
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, stream_handle()))
+    return y
+
+
+def ssd_stem_nhwc(x4, w0_packed, b0, wd_taps, bd, w1_packed, b1):
+    """SSDLite features.0.0 + features.0.1 fused (csrc/layers.hip ssd_stem_kernel): x4 the NHWC4
+    preprocessed images, weights packed by plan.pack_conv_weight / pack_dw_weight (folded BN)."""
+    _need_cuda(x4, w0_packed, b0, wd_taps, bd, w1_packed, b1)
+    B, H, W, _ = x4.shape
+    y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, 16), dtype=torch.float32, device=x4.device)
+    check(lib().edgedet_ssd_stem(_ptr(x4), B, H, W, _ptr(w0_packed), w0_packed.shape[1], _ptr(b0), _ptr(wd_taps),
+                                 _ptr(bd), _ptr(w1_packed), w1_packed.shape[1], _ptr(b1), _ptr(y), stream_handle()))
     return y
 
 

@@ -66,7 +66,8 @@ enum {
     EDGEDET_OP_SSD_POSTPROCESS = 17,/* per image: class top-k pool, global-order greedy NMS, [:N]      */
     EDGEDET_OP_GN_STATS = 18,     /* GroupNorm statistics -> per (image, channel) scale / shift       */
     EDGEDET_OP_RETINA_SELECT = 19,/* RetinaNet per (image, level): sigmoid > t, top-k, decode, clip   */
-    EDGEDET_OP_RETINA_CLASS_NMS = 20 /* RetinaNet per (image, class): NMS over the level candidates  */
+    EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
+    EDGEDET_OP_SSD_STEM = 21      /* SSDLite features.0.0 + features.0.1 in one pass                  */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,
@@ -154,6 +155,15 @@ int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream)
 int edgedet_mbconv_front(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w1,
                          int64_t w1_ld, const float* b1, int32_t act1, int64_t C, const float* w,
                          const float* bias, int32_t K, int32_t stride, int32_t act, float* y, void* stream);
+/*
+ * SSDLite stem + first block in one pass: y = proj(relu(dw3x3(s))) + b1 + s with
+ * s = hardswish(conv3x3_s2(x) + b0) (torchvision mobilenet_v3_large features.0.0 and .0.1, folded BN).
+ * x NHWC4 [B,H,W,4] (the preprocessed image); w0 [16][ld0] packed (kh, kw, ci); wd [9][16];
+ * w1 [16][ld1]; y [B,(H+1)/2,(W+1)/2,16].
+ */
+int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W, const float* w0, int64_t ld0,
+                     const float* b0, const float* wd, const float* bd, const float* w1, int64_t ld1,
+                     const float* b1, float* y, void* stream);
 /* LDS bytes edgedet_mbconv_front needs for (K, stride, Cin); 0 if (K, stride) is not supported. */
 int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin);
 /* Depthwise conv2d (+ folded BN + act).  x NHWC [B,H,W,C]; w [KH*KW][C]; bias [C]. */

@@ -121,6 +121,31 @@ def test_dwconv_se_partial_sums(B, H, W, C, k, s, act):
     assert torch.allclose(tot, ref.sum((2, 3)), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 320, 320), (1, 37, 50), (3, 2, 3), (1, 33, 31)])
+def test_ssd_stem_matches_torch(B, H, W):
+    """SSDLite features.0.0 + features.0.1 fused (csrc/layers.hip ssd_stem_kernel) against torch fp32:
+    hardswish(conv3x3 s2) -> relu(depthwise 3x3) -> 1x1 projection + residual."""
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight, pack_dw_weight
+    g = torch.Generator().manual_seed(H * W + B)
+    x = torch.randn(B, 3, H, W, generator=g)
+    w0 = torch.randn(16, 3, 3, 3, generator=g) / 27 ** 0.5
+    b0 = torch.randn(16, generator=g) * 0.1
+    wd = torch.randn(16, 1, 3, 3, generator=g) / 3
+    bd = torch.randn(16, generator=g) * 0.1
+    w1 = torch.randn(16, 16, 1, 1, generator=g) / 4
+    b1 = torch.randn(16, generator=g) * 0.1
+    s = F.hardswish(F.conv2d(x, w0, b0, 2, 1))
+    ref = F.conv2d(F.relu(F.conv2d(s, wd, bd, 1, 1, 1, 16)), w1, b1) + s
+    x4 = torch.cat([x, torch.zeros(B, 1, H, W)], 1).permute(0, 2, 3, 1).contiguous()
+    dev = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    got = ops.ssd_stem_nhwc(x4.to(DEV), dev(pack_conv_weight(w0.numpy(), 4)[0]), b0.to(DEV),
+                            dev(pack_dw_weight(wd.numpy())), bd.to(DEV), dev(pack_conv_weight(w1.numpy())[0]),
+                            b1.to(DEV))
+    err = (got.permute(0, 3, 1, 2).cpu() - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
 @pytest.mark.parametrize("B,H,W,Cin,C,k,s,act1,act2", [
     (2, 160, 160, 16, 64, 3, 2, "RE", "RE"),   # SSDLite block 0.2 (expand 16 -> 64, dw 3x3 s2)
     (2, 80, 80, 24, 72, 3, 1, "RE", "RE"),     # block 0.3

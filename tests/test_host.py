@@ -154,9 +154,13 @@ def test_ssd_plan_lowering():
     # convs: stem 1 + blocks 0-11 (block 0 has no expansion: 1 + 11*2) + C4 split 2 + blocks 13-14 (2*2)
     #        + last 1 + extras 4*2 + head 6*2
     n_conv = kinds.count(ops.CONV)
+    # with the fused stem (SSD_STEM = features.0.0 + block 0's depthwise and projection) one
+    # depthwise and two convs fewer
     n_dw = kinds.count(ops.DWCONV)
-    assert n_dw == 15 + 4 + 12
-    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12
+    stem = kinds.count(ops.SSD_STEM)
+    assert stem == (1 if models.SSD_STEM_FUSE else 0)
+    assert n_dw == 15 + 4 + 12 - stem
+    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12 - 2 * stem
     assert kinds.count(ops.SE_FC) == 8
     assert m.grids == [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
     for op in P.ops:
