@@ -621,6 +621,20 @@ int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStr
 constexpr int SE1_BB = 8, SE1_SB = 8, SE2_BB = 8, SE2_SCH = 128;
 constexpr int SE_CMAX = 1024, SE_SMAX = 512;
 
+// mean over the squeeze partial sums pp[k * C], k < parts, summed in k order (loads issued four at
+// a time; only the `parts` that exist are read).
+__device__ __forceinline__ float squeeze_mean(const float* __restrict__ pp, int C, int parts, float inv) {
+    float acc = 0.f;
+    for (int k0 = 0; k0 < parts; k0 += 4) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = pp[(int64_t)(k0 + u < parts ? k0 + u : parts - 1) * C];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += k0 + u < parts ? v[u] : 0.f;
+    }
+    return acc * inv;
+}
+
 __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ part, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, float* __restrict__ hidden, int B,
                                                      int C, int S, int HW, int parts) {
@@ -631,14 +645,7 @@ __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ p
     const float inv = 1.f / (float)HW;
     for (int t = threadIdx.x; t < nb * C; t += 256) {
         const int bl = t / C, c = t - bl * C;
-        const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
-        float v[SE_PARTS];
-#pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)(k < parts ? k : parts - 1) * C];  // independent loads
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) acc += k < parts ? v[k] : 0.f;
-        ms[t] = acc * inv;
+        ms[t] = squeeze_mean(part + ((int64_t)(b0 + bl) * parts) * C + c, C, parts, inv);
     }
     for (int t = threadIdx.x; t < ns * C; t += 256) ws[t] = w1[(int64_t)s0 * C + t];
     __syncthreads();
@@ -651,7 +658,8 @@ __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ p
     if (bl < nb && sl < ns) {
         const float* mr = ms + bl * C;
         const float* wr = ws + sl * C;
-        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);
+#pragma unroll 8
+        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);  // unrolled: the loads issue together
     }
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
@@ -680,6 +688,7 @@ __global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ h
             ws[t] = c < nc ? w2t[(int64_t)(j0 + j) * C + c0 + c] : 0.f;
         }
         __syncthreads();
+#pragma unroll 8
         for (int j = 0; j < nj; ++j) {
             const float wv = ws[j * 64 + cl];
             a0 = fmaf(wv, h0[j0 + j], a0);
@@ -711,14 +720,7 @@ __global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__
     const float inv = 1.f / (float)HW;
     for (int t = threadIdx.x; t < nb * C; t += 512) {
         const int bl = t / C, c = t - bl * C;
-        const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
-        float v[SE_PARTS];
-#pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) v[k] = pp[(int64_t)(k < parts ? k : parts - 1) * C];
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < SE_PARTS; ++k) acc += k < parts ? v[k] : 0.f;
-        ms[t] = acc * inv;
+        ms[t] = squeeze_mean(part + ((int64_t)(b0 + bl) * parts) * C + c, C, parts, inv);
     }
     __syncthreads();
     // fc1: output (s, b) by a group of 4 lanes over C quarters (same order as se_fc1_kernel)
@@ -730,7 +732,8 @@ __global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__
         const float* wr = w1 + (int64_t)sl * C;
         const float* mr = ms + bl * C;
         float acc = 0.f;
-        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);
+#pragma unroll 8
+        for (int c = c0; c < c1; ++c) acc = fmaf(wr[c], mr[c], acc);  // unrolled: the loads issue together
         acc += __shfl_xor(acc, 1);
         acc += __shfl_xor(acc, 2);
         if (h == 0) {
@@ -745,6 +748,7 @@ __global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__
         float a[SE_FB];
 #pragma unroll
         for (int q = 0; q < SE_FB; ++q) a[q] = 0.f;
+#pragma unroll 8
         for (int j = 0; j < S; ++j) {
             const float wv = w2t[(int64_t)j * C + c];
 #pragma unroll

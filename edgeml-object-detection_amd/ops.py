@@ -44,7 +44,8 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds", "edgedet_ssd_stem")
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds", "edgedet_ssd_stem",
+           "edgedet_mlp_state_size", "edgedet_mlp_fit", "edgedet_mlp_predict")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -87,6 +88,12 @@ def lib():
                                     _i32, _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
     L.edgedet_mbconv_front_lds.argtypes = [_i32, _i32, _i64]
+    L.edgedet_mlp_state_size.argtypes = [_i32, _vp]
+    L.edgedet_mlp_state_size.restype = ctypes.c_int64
+    L.edgedet_mlp_fit.argtypes = [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _i32, _i32, ctypes.c_float, ctypes.c_float, _vp, _i32, ctypes.c_float, _i32,
+                                  ctypes.c_float, ctypes.c_uint64, _vp]
+    L.edgedet_mlp_predict.argtypes = [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _vp]
     L.edgedet_ssd_stem.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]
     L.edgedet_mbconv_front_lds.restype = ctypes.c_int64
     L.edgedet_mbconv_front.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32, _i32,
@@ -105,7 +112,8 @@ def lib():
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
                  "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_ssd_stem"):
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_ssd_stem", "edgedet_mlp_fit",
+                 "edgedet_mlp_predict"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
     return L

@@ -164,6 +164,27 @@ int edgedet_mbconv_front(const float* x, int64_t B, int64_t H, int64_t W, int64_
 int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W, const float* w0, int64_t ld0,
                      const float* b0, const float* wd, const float* bd, const float* w1, int64_t ld1,
                      const float* b1, float* y, void* stream);
+/*
+ * ORIE estimator (regression.py:242-355 fit_CNN on the stage-24 features, lib/nn_model.py:28-112
+ * with linear stacks only): an MLP dims[0] -> ... -> dims[L] = 1 whose hidden layers are Linear,
+ * BatchNorm1d, ReLU, Dropout(dropout); MSE loss (reward-weighted when `weighted`), Adam(lr,
+ * weight_decay), MultiStepLR(milestones, gamma), `batch` rows in index order, a test pass on the
+ * validation rows after every epoch.  One workgroup per fold f trains on rows tr_idx[tr_off[f] ..
+ * tr_off[f+1]) with targets y[f][.] and tests on va_idx[va_off[f] .. va_off[f+1]).  State vectors
+ * ([F][edgedet_mlp_state_size]: per layer W, b, and for hidden layers gamma, beta; then the running
+ * mean / var) start from init; best (lowest test loss) and last are written; adam is [F][2 * params]
+ * scratch; train_loss / test_loss are [F][epochs].  dims and milestones are host arrays.
+ */
+int64_t edgedet_mlp_state_size(int32_t L, const int32_t* dims);
+int edgedet_mlp_fit(const float* x, int64_t N, int64_t D0, const float* y, const int32_t* tr_idx,
+                    const int64_t* tr_off, const int32_t* va_idx, const int64_t* va_off, int32_t folds, int32_t L,
+                    const int32_t* dims, const float* init, float* best, float* last, float* adam,
+                    float* train_loss, float* test_loss, int32_t epochs, int32_t batch, float lr, float gamma,
+                    const int32_t* milestones, int32_t n_milestones, float weight_decay, int32_t weighted,
+                    float dropout, uint64_t seed, void* stream);
+/* Eval-mode forward of a trained state (running statistics, no dropout): out[r] = net(x[idx[r]]). */
+int edgedet_mlp_predict(const float* x, int64_t D0, const int32_t* idx, int64_t n, int32_t L, const int32_t* dims,
+                        const float* state, float* out, void* stream);
 /* LDS bytes edgedet_mbconv_front needs for (K, stride, Cin); 0 if (K, stride) is not supported. */
 int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin);
 /* Depthwise conv2d (+ folded BN + act).  x NHWC [B,H,W,C]; w [KH*KW][C]; bias [C]. */

@@ -247,3 +247,34 @@ def test_mbconv_front_lds_formula_matches_library():
         ipp = ((7 * s + k) ** 2 + 31) // 32 * 32
         assert L.edgedet_mbconv_front_lds(k, s, cin) == 4 * (ipp * (cin + 4) + 32 * (cin + 4) + ipp * 36)
     assert L.edgedet_mbconv_front_lds(7, 1, 16) == 0
+
+
+def test_estimator_state_layout_matches_library():
+    """edgeml_amd.estimator.MlpSpec and csrc/estimator.hip mlp_layout agree on the state size."""
+    import ctypes
+    from edgeml_amd import estimator, ops
+    for dims in ([145, 16, 16, 16, 16, 1], [205, 16, 16, 16, 16, 1], [8, 1], [30, 64, 1]):
+        spec = estimator.MlpSpec(dims)
+        arr = (ctypes.c_int32 * len(dims))(*dims)
+        assert ops.lib().edgedet_mlp_state_size(len(dims) - 1, arr) == spec.ns
+    spec = estimator.MlpSpec([145, 16, 16, 16, 16, 1])
+    assert spec.np == 145 * 16 + 16 + 2 * 16 + 3 * (16 * 16 + 16 + 2 * 16) + 16 + 1
+
+
+def test_estimator_host_helpers_follow_the_reference():
+    """parse_path (lib/utils.py:8-22, absolute paths lose their root as os.path.join(*parts) does),
+    the rank normalisation (regression.py:431-434) and the init bounds (kaiming_uniform_)."""
+    import numpy as np
+    from edgeml_amd import estimator
+    assert estimator.parse_path("runs/est") == ("runs/est_best", "runs/est_last")
+    assert estimator.parse_path("/tmp/x/est") == ("tmp/x/est_best", "tmp/x/est_last")
+    assert estimator.parse_path("") == ("", "")
+    tr = np.array([0.3, 0.1, 0.2, 0.5])
+    a, b = estimator.normalize_rewards(tr, np.array([0.25, 0.6]))
+    np.testing.assert_array_equal(a, [0.75, 0.25, 0.5, 1.0])
+    np.testing.assert_array_equal(b, [0.5, 1.0])
+    spec = estimator.MlpSpec([145, 16, 1])
+    s = spec.init_state(np.random.default_rng(0))
+    w = spec.unpack(s)["linear_stacks.0.0.weight"]
+    assert np.abs(w).max() <= np.sqrt(6 / 145) and np.abs(w).max() > 0.9 * np.sqrt(6 / 145)
+    assert (spec.unpack(s)["linear_stacks.0.1.running_var"] == 1).all()

@@ -1,4 +1,3 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py tests/test_gpu_pipeline.py -m gpu -x -q --timeout 120 --timeout-method thread -k "stem or ssd or SSD or voc" 2>&1 | tail -2 || exit 1
-timeout -k 10 200 python bench.py --model ssd --steps 20 --warmup 5 --dump-ops gpurun_out/ops_ssd_stem.json 2>&1 | tail -1 | cut -c1-300 || exit 1
-EDGEDET_SSD_STEM_FUSE=0 timeout -k 10 200 python bench.py --model ssd --steps 20 --warmup 5 2>&1 | tail -1 | cut -c1-300
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py -m gpu -x -q --timeout 120 --timeout-method thread -k "se_ or ssd or SSD" 2>&1 | tail -2 || exit 1
+timeout -k 10 200 python bench.py --model ssd --steps 20 --warmup 5 --dump-ops gpurun_out/ops_ssd_se.json 2>&1 | tail -1 | cut -c1-300 || exit 1
