@@ -621,18 +621,59 @@ int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStr
 constexpr int SE1_BB = 8, SE1_SB = 8, SE2_BB = 8, SE2_SCH = 128;
 constexpr int SE_CMAX = 1024, SE_SMAX = 512;
 
-// mean over the squeeze partial sums pp[k * C], k < parts, summed in k order (loads issued four at
-// a time; only the `parts` that exist are read).
-__device__ __forceinline__ float squeeze_mean(const float* __restrict__ pp, int C, int parts, float inv) {
-    float acc = 0.f;
-    for (int k0 = 0; k0 < parts; k0 += 4) {
-        float v[4];
+// LDS staging with SE_U independent loads in flight per thread (a plain strided loop waits for
+// every load before issuing the next: one memory round trip per element, which dominated these
+// latency-bound kernels).  dst[t] = src(t) for t < n; with ACC, dst[t] += src(t).
+constexpr int SE_U = 8;
+template <bool ACC, typename F>
+__device__ __forceinline__ void se_stage(float* dst, int n, F src) {
+    for (int base = threadIdx.x; base < n; base += 256 * SE_U) {
+        float v[SE_U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = pp[(int64_t)(k0 + u < parts ? k0 + u : parts - 1) * C];
+        for (int u = 0; u < SE_U; ++u) {
+            const int t = base + 256 * u;
+            v[u] = t < n ? src(t) : 0.f;
+        }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc += k0 + u < parts ? v[u] : 0.f;
+        for (int u = 0; u < SE_U; ++u) {
+            const int t = base + 256 * u;
+            if (t < n) dst[t] = ACC ? dst[t] + v[u] : v[u];
+        }
     }
-    return acc * inv;
+}
+
+// ms[bl * C + c] = mean over the squeeze partial sums of image b0 + bl, summed in part order; the
+// loads of SE_U elements x 4 parts are issued together.
+__device__ __forceinline__ void se_stage_means(float* ms, const float* __restrict__ part, int b0, int nb, int C,
+                                               int parts, float inv) {
+    const int n = nb * C;
+    for (int base = threadIdx.x; base < n; base += 256 * SE_U) {
+        const float* src[SE_U];
+        float acc[SE_U];
+#pragma unroll
+        for (int u = 0; u < SE_U; ++u) {
+            const int t = min(base + 256 * u, n - 1);
+            const int bl = t / C, c = t - bl * C;
+            src[u] = part + (int64_t)(b0 + bl) * parts * C + c;
+            acc[u] = 0.f;
+        }
+        for (int k0 = 0; k0 < parts; k0 += 4) {
+            float v[SE_U][4];
+#pragma unroll
+            for (int u = 0; u < SE_U; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[u][q] = src[u][(int64_t)min(k0 + q, parts - 1) * C];
+#pragma unroll
+            for (int u = 0; u < SE_U; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[u] += k0 + q < parts ? v[u][q] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < SE_U; ++u) {
+            const int t = base + 256 * u;
+            if (t < n) ms[t] = acc[u] * inv;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ part, const float* __restrict__ w1,
@@ -643,11 +684,8 @@ __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ p
     const int s0 = blockIdx.x * SE1_SB, b0 = blockIdx.y * SE1_BB;
     const int nb = min(SE1_BB, B - b0), ns = min(SE1_SB, S - s0);
     const float inv = 1.f / (float)HW;
-    for (int t = threadIdx.x; t < nb * C; t += 256) {
-        const int bl = t / C, c = t - bl * C;
-        ms[t] = squeeze_mean(part + ((int64_t)(b0 + bl) * parts) * C + c, C, parts, inv);
-    }
-    for (int t = threadIdx.x; t < ns * C; t += 256) ws[t] = w1[(int64_t)s0 * C + t];
+    se_stage_means(ms, part, b0, nb, C, parts, inv);  // each thread rewrites only its own elements
+    se_stage<false>(ws, ns * C, [&](int t) { return w1[(int64_t)s0 * C + t]; });
     __syncthreads();
     // 64 outputs (bl = o & 7, sl = o >> 3), 4 threads each over C quarters
     const int o = threadIdx.x >> 2, h = threadIdx.x & 3;
@@ -676,17 +714,17 @@ __global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ h
     __shared__ float ws[SE2_SCH * 64];
     const int c0 = blockIdx.x * 64, b0 = blockIdx.y * SE2_BB;
     const int nb = min(SE2_BB, B - b0), nc = min(64, C - c0);
-    for (int t = threadIdx.x; t < nb * S; t += 256) hs[t] = hidden[(int64_t)b0 * S + t];
+    se_stage<false>(hs, nb * S, [&](int t) { return hidden[(int64_t)b0 * S + t]; });
     const int cl = threadIdx.x & 63, bp = threadIdx.x >> 6;  // images bp and bp + 4
     float a0 = 0.f, a1 = 0.f;
     const float* h0 = hs + bp * S;
     const float* h1 = hs + (bp + 4) * S;
     for (int j0 = 0; j0 < S; j0 += SE2_SCH) {
         const int nj = min(SE2_SCH, S - j0);
-        for (int t = threadIdx.x; t < nj * 64; t += 256) {
+        se_stage<false>(ws, nj * 64, [&](int t) {
             const int j = t >> 6, c = t & 63;
-            ws[t] = c < nc ? w2t[(int64_t)(j0 + j) * C + c0 + c] : 0.f;
-        }
+            return c < nc ? w2t[(int64_t)(j0 + j) * C + c0 + c] : 0.f;
+        });
         __syncthreads();
 #pragma unroll 8
         for (int j = 0; j < nj; ++j) {
@@ -718,9 +756,12 @@ __global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__
     const int b0 = blockIdx.x * SE_FB;
     const int nb = min(SE_FB, B - b0);
     const float inv = 1.f / (float)HW;
-    for (int t = threadIdx.x; t < nb * C; t += 512) {
+    for (int t = threadIdx.x; t < nb * C; t += 512) {  // nb * C <= 4 * 1024: at most 8 rounds
         const int bl = t / C, c = t - bl * C;
-        ms[t] = squeeze_mean(part + ((int64_t)(b0 + bl) * parts) * C + c, C, parts, inv);
+        const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
+        float acc = 0.f;
+        for (int k = 0; k < parts; ++k) acc += pp[(int64_t)k * C];
+        ms[t] = acc * inv;
     }
     __syncthreads();
     // fc1: output (s, b) by a group of 4 lanes over C quarters (same order as se_fc1_kernel)

@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?"; tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -u tools/estimator_bench.py > gpurun_out/estimator_bench.log 2>&1; echo "est rc=$?"; cat gpurun_out/estimator_bench.log | grep -v amdgpu.ids
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py -m gpu -x -q --timeout 120 --timeout-method thread -k "se_ or ssd or SSD" 2>&1 | tail -2 || exit 1
+timeout -k 10 200 python bench.py --model ssd --steps 30 --warmup 5 --dump-ops gpurun_out/ops_ssd_se.json 2>&1 | tail -1 | cut -c1-300 || exit 1
