@@ -88,4 +88,22 @@ __device__ __forceinline__ float key_float(uint32_t k) {
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Block-wide copy into LDS with U independent loads in flight per thread: dst[t] = src(t), t < n.
+// (A plain strided loop issues one load per iteration and waits for it before the store: one memory
+// round trip per element, the dominant cost of small latency-bound kernels.)
+template <int NT, int U, typename T, typename F>
+__device__ __forceinline__ void stage_lds(T* dst, int n, F src) {
+    for (int base = threadIdx.x; base < n; base += NT * U) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = base + NT * u;
+            v[u] = src(t < n ? t : n - 1);  // clamped index: every load is issued unconditionally
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + NT * u < n) dst[base + NT * u] = v[u];
+    }
+}
+
 }  // namespace edgedet

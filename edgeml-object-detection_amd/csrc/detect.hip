@@ -88,9 +88,13 @@ __global__ void __launch_bounds__(256) ssd_scores_kernel(const float* __restrict
     const int na = min(64, A - a0);
     const int ld = (NC & 1) ? NC : NC + 1;
     const float* src = logits + ((int64_t)b * A + a0) * NC;
-    for (int e = threadIdx.x; e < na * NC; e += 256) {
-        const int a = e / NC, c = e - a * NC;
-        tile[a * ld + c] = src[e];
+    if (ld == NC) {
+        stage_lds<256, 8>(tile, na * NC, [&](int e) { return src[e]; });
+    } else {
+        for (int e = threadIdx.x; e < na * NC; e += 256) {
+            const int a = e / NC, c = e - a * NC;
+            tile[a * ld + c] = src[e];
+        }
     }
     __syncthreads();
     const int a = threadIdx.x & 63, q = threadIdx.x >> 6;

@@ -298,12 +298,21 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
     const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
     const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
     const float* xb = p.x + (int64_t)b * p.H * p.W * 4;
-    for (int v = tid; v < STEM_XH * STEM_XH; v += 256) {
-        const int ih = xh0 + v / STEM_XH, iw = xw0 + v % STEM_XH;
-        f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-            xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * 4);
-        *reinterpret_cast<f32x4*>(xs + 4 * v) = xv;
+    {  // all of a thread's input pixels in flight at once (one memory round trip)
+        constexpr int R = (STEM_XH * STEM_XH + 255) / 256;
+        f32x4 xv[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int v = tid + 256 * r;
+            const int ih = xh0 + v / STEM_XH, iw = xw0 + v % STEM_XH;
+            const bool in = v < STEM_XH * STEM_XH && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const float* src = xb + (in ? ((int64_t)ih * p.W + iw) * 4 : 0);  // clamped: loads stay unconditional
+            xv[r] = *reinterpret_cast<const f32x4*>(src);
+            if (!in) xv[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (tid + 256 * r < STEM_XH * STEM_XH) *reinterpret_cast<f32x4*>(xs + 4 * (tid + 256 * r)) = xv[r];
     }
     __syncthreads();
     for (int v = tid; v < STEM_SH * STEM_SH; v += 256) {
