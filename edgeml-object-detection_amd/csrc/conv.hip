@@ -720,6 +720,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 #ifndef X6B_PIPE
 #define X6B_PIPE 1
 #endif
+#ifndef X6B_GLDS
+#define X6B_GLDS 1
+#endif
 constexpr int BK6B = 32;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
@@ -732,6 +735,7 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 template <bool XF, bool UT, bool PS>
 __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
+    constexpr bool GL = X6B_GLDS && X6B_PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
     constexpr int WM = 4, WN = 2, TM = 2, TN = 2, NT = 512;
     constexpr int BM = 256, BN = 128;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
@@ -805,7 +809,19 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         uint4 b[3];
     };
     const int64_t x3plane = (int64_t)p.B * p.H * p.W * p.Cin;
-    auto load_stage = [&](Regs& R, int k0) {
+    auto load_stage = [&](Regs& R, int k0, int bbuf) {
+        if constexpr (GL) {
+            // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
+            // -> the 16-B slot l of the block); the swizzle is applied on the source address
+            const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 2) & 3);
+            const int n = n0 + row < p.Cout ? n0 + row : p.Cout - 1;
+            const unsigned short* src = reinterpret_cast<const unsigned short*>(p.w3) + (int64_t)n * p.Kpad + k0 + 8 * lc;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + pl * wplane),
+                    (__attribute__((address_space(3))) void*)(Bs + bbuf * 3 * PB + pl * PB + 16 * wid * BK6B), 16, 0, 0);
+        }
         if constexpr (PS) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
@@ -854,9 +870,11 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
                 R.a[j] = v;
             }
         }
+        if constexpr (!GL) {
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-            R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
+            for (int pl = 0; pl < 3; ++pl)
+                R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
+        }
     };
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
@@ -881,8 +899,9 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             }
         }
         const int o = swz64(b_row, b_chunk);
+        if constexpr (!GL)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = R.b[pl];
+            for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = R.b[pl];
     };
 
     floatx16 acc[TM][TN];
@@ -945,34 +964,31 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // the read latency after each barrier.
     Regs r0;
     Frags F0, F1;
-    load_stage(r0, 0);
+    load_stage(r0, 0, 0);
     store_stage(r0, 0);
     __syncthreads();
-    if (nk > 1) load_stage(r0, BK6B);
+    if (nk > 1) load_stage(r0, BK6B, 1);
     read_frags(F0, 0, 0);
     mfmas(F0);
     read_frags(F1, 0, 1);
     if (nk > 1) store_stage(r0, 1);
     __syncthreads();
-#ifndef X6B_DIAG
-#define X6B_DIAG 0  // timing ablations (wrong results): 1 no barrier, 2 no global loads, 4 no LDS reads, 8 no LDS writes
-#endif
     for (int kc = 1; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (!(X6B_DIAG & 2) && kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B);
-        if (!(X6B_DIAG & 4)) read_frags(F0, buf, 0);
+        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B, buf ^ 1);
+        read_frags(F0, buf, 0);
         __builtin_amdgcn_sched_barrier(0);  // issue the reads before the MFMAs that hide them
         mfmas(F1);
 #if X6B_PIPE == 2
-        if (!(X6B_DIAG & 8)) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+        store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
         mfmas(F0);
-        if (!(X6B_DIAG & 4)) read_frags(F1, buf, 1);
+        read_frags(F1, buf, 1);
 #else
         mfmas(F0);
-        if (!(X6B_DIAG & 4)) read_frags(F1, buf, 1);
-        if (!(X6B_DIAG & 8)) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+        read_frags(F1, buf, 1);
+        store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
 #endif
-        if (!(X6B_DIAG & 1)) __syncthreads();
+        __syncthreads();
     }
     mfmas(F1);
 #elif X6B_PF == 2
@@ -980,12 +996,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
     // time to land.
     Regs r0, r1;
-    load_stage(r0, 0);
+    load_stage(r0, 0, 0);
     store_stage(r0, 0);
-    if (nk > 1) load_stage(r1, BK6B);
+    if (nk > 1) load_stage(r1, BK6B, 1);
     __syncthreads();
     auto step = [&](int kc, Regs& hold, Regs& next) {
-        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6B);
+        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6B, kc & 1);  // (no LDS-DMA with two register stages)
         compute(kc & 1);
         if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
         __syncthreads();
@@ -996,12 +1012,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     }
 #else
     Regs r0;
-    load_stage(r0, 0);
+    load_stage(r0, 0, 0);
     store_stage(r0, 0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B);
+        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B, buf ^ 1);
         compute(buf);
         if (kc + 1 < nk) store_stage(r0, buf ^ 1);
         __syncthreads();
