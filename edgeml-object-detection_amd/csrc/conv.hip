@@ -724,6 +724,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 #define X6B_GLDS 1
 #endif
 constexpr int BK6B = 32;
+constexpr int X3Z = 32;  // leading zero elements of a pre-split scratch (16-B aligned planes follow)
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
 
@@ -765,7 +766,10 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int n0 = (bid % nnt) * BN;
 
     const int c8 = tid & 7;  // f32x4 column of the 32-deep stage
-    const int a_row0 = PS ? tid >> 2 : tid >> 3;
+    // A rows of this thread: with LDS-DMA of the pre-split planes (PS && GL) wave w owns rows
+    // 32w .. 32w+31 (two 1-KiB blocks, lane l -> 16-B slot l); otherwise rows step by AROWS
+    const int a_row0 = PS ? (GL ? 32 * wid + (lane >> 2) : tid >> 2) : tid >> 3;
+    constexpr int AST = PS && GL ? 16 : AROWS;
     // pixel / batch strides of the A source: the fp32 input, or the dense bf16 planes
     const int x_ps = PS ? p.Cin : p.x_pstride;
     const int64_t x_bs = PS ? (int64_t)p.H * p.W * p.Cin : p.x_bstride;
@@ -773,7 +777,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     int a_ih0[AJ], a_iw0[AJ], a_b[AJ];
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
-        const int m = m0 + a_row0 + AROWS * j;
+        const int m = m0 + a_row0 + AST * j;
         if (m < p.M && p.lin_x) {
             a_b[j] = XF ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
             a_base[j] = (int64_t)m * x_ps;
@@ -809,6 +813,8 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         uint4 b[3];
     };
     const int64_t x3plane = (int64_t)p.B * p.H * p.W * p.Cin;
+    // x3 scratch: X3Z zero elements (the source of padding taps under LDS-DMA), then the three planes
+    const unsigned short* x3 = reinterpret_cast<const unsigned short*>(p.x3);
     auto load_stage = [&](Regs& R, int k0, int bbuf) {
         if constexpr (GL) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
@@ -826,15 +832,34 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
             const int kw = tap - kh * p.KW;
-            const unsigned short* xt = reinterpret_cast<const unsigned short*>(p.x3) +
-                                       (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin) + 8 * (tid & 3);
+            if constexpr (GL) {
+                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin);
 #pragma unroll
-            for (int j = 0; j < AJ; ++j) {
-                const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-                const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+                for (int j = 0; j < AJ; ++j) {
+                    const int row = a_row0 + AST * j;
+                    const int lc = (lane & 3) ^ ((row >> 2) & 3);  // swizzle on the source address
+                    const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                    const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-                    R.a3[j][pl] = ok ? *reinterpret_cast<const uint4*>(xt + pl * x3plane + a_base[j]) : uint4{0u, 0u, 0u, 0u};
+                    for (int pl = 0; pl < 3; ++pl)
+                        __builtin_amdgcn_global_load_lds(
+                            (const __attribute__((address_space(1))) void*)(ok ? xt + pl * x3plane + a_base[j] + 8 * lc
+                                                                               : x3),
+                            (__attribute__((address_space(3))) void*)(As + bbuf * 3 * PA + pl * PA +
+                                                                      (32 * wid + 16 * j) * BK6B),
+                            16, 0, 0);
+                }
+            } else {
+                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin) + 8 * (tid & 3);
+#pragma unroll
+                for (int j = 0; j < AJ; ++j) {
+                    const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                    const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        R.a3[j][pl] =
+                            ok ? *reinterpret_cast<const uint4*>(xt + pl * x3plane + a_base[j]) : uint4{0u, 0u, 0u, 0u};
+                }
             }
         } else if constexpr (UT) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
@@ -879,7 +904,9 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
-        if constexpr (PS) {
+        if constexpr (PS && GL) {
+            // A arrived by LDS-DMA
+        } else if constexpr (PS) {
 #pragma unroll
             for (int j = 0; j < AJ; ++j) {
                 const int o = swz64(a_row0 + AROWS * j, tid & 3);
@@ -1034,7 +1061,9 @@ template <bool XF>
 __global__ void __launch_bounds__(256) split_act_kernel(ConvParams p) {
     const int C8 = p.Cin >> 3;
     const int64_t HW = (int64_t)p.H * p.W, npix = (int64_t)p.B * HW, n = npix * C8;
-    unsigned short* out = reinterpret_cast<unsigned short*>(p.x3);
+    unsigned short* out = reinterpret_cast<unsigned short*>(p.x3) + X3Z;
+    if (blockIdx.x == 0 && threadIdx.x < X3Z / 8)  // the zero page padding taps read under LDS-DMA
+        reinterpret_cast<uint4*>(p.x3)[threadIdx.x] = uint4{0u, 0u, 0u, 0u};
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t pix = i / C8;
         const int c = (int)(i - pix * C8) * 8;

@@ -190,7 +190,7 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
-    x3 = torch.empty(3 * B * H * W * Cin, dtype=torch.int16, device=x.device) if presplit else None
+    x3 = torch.empty(3 * B * H * W * Cin + 32, dtype=torch.int16, device=x.device) if presplit else None
     if tile == 0 and in_scale is None:
         if x3 is not None:
             check(lib().edgedet_conv2d_x3(_ptr(x), _ptr(x3), B, H, W, Cin, _ptr(w_packed), _ptr(w3), _ptr(bias), cout,

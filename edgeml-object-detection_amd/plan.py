@@ -353,5 +353,5 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
     # the extra pass costs more than the in-loop split (box head 2.48 -> 2.60 ms)
     xf = in_scale is not None or in_shift is not None or in_relu
     if CONV_PRESPLIT and xf and w3 is not None and C % 32 == 0 and op.i[23] in (0, 25):
-        op.p[8] = plan.x3_scratch(3 * B * H * W * C)
+        op.p[8] = plan.x3_scratch(3 * B * H * W * C + 32)  # 32 leading zeros (csrc/conv.hip X3Z)
     return plan.add(op)

@@ -133,7 +133,7 @@ int edgedet_conv2d_ex(const float* x, int64_t B, int64_t H, int64_t W, int64_t C
                       int32_t stride, int32_t pad, int32_t act, const float* res, float* y, int32_t tile,
                       void* stream);
 /*
- * edgedet_conv2d_ex with a caller-owned scratch x3 of 3 * B*H*W*Cin uint16: when the 256 x 128
+ * edgedet_conv2d_ex with a caller-owned scratch x3 of 3 * B*H*W*Cin + 32 uint16: when the 256 x 128
  * bf16x6 tile runs (tile 25, Cin % 32 == 0) the input is split into three bf16 planes once, by a
  * separate pass into x3, instead of inside every N tile of the GEMM.  Results are bit-identical to
  * edgedet_conv2d_ex; x3 may be null (then this is edgedet_conv2d_ex).
