@@ -162,6 +162,8 @@ def op_work(op):
         return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
     if k in (O.FORK, O.JOIN):
         return "lanes", 0.0, 0.0
+    if k == O.MEMSET:  # zeroing the output of a split-K conv
+        return "conv", 0.0, float(i[0])
     return f"kind{k}", 0.0, 0.0
 
 

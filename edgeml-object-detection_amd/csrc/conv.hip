@@ -99,6 +99,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx16 (&ac
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j][r] = (acc[i][j][r] + bj[j]) + rrow[nc[j]];
             }
+    } else if (p.ksplit > 1) {
+        // two K halves meet in y (zeroed by the plan): the first adds the bias; a + b == b + a in
+        // IEEE arithmetic, so the result does not depend on which half lands first
+        const bool first = (blockIdx.x & 1) == 0;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = row0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                float* yrow = p.y + conv_row_offset(p, m < p.M ? m : p.M - 1, false);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (m < p.M && col0 + j * 32 + l32 < p.Cout)
+                        atomicAdd(yrow + nc[j], first ? acc[i][j][r] + bj[j] : acc[i][j][r]);
+            }
+        return;
     } else {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -757,7 +773,8 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int nmt = (p.M + BM - 1) / BM;
     const int nnt = (p.Cout + BN - 1) / BN;
     const int nwg = nmt * nnt;
-    int bid = blockIdx.x;
+    const int ksp = p.ksplit > 1 ? 2 : 1;  // split-K: block 2t + s takes K half s of tile t
+    int bid = blockIdx.x / ksp;
     {
         const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
@@ -939,7 +956,10 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nk = p.Kpad / BK6B;
+    const int nk_all = p.Kpad / BK6B;
+    const int kbeg = ksp > 1 ? (blockIdx.x & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
+    const int nk = ksp > 1 ? ((blockIdx.x & 1) ? nk_all - kbeg : (nk_all + 1) / 2) : nk_all;
+    const int kofs = kbeg * BK6B;
     const int h = lane >> 5;
     const int l32 = lane & 31;
     struct Frags {
@@ -991,10 +1011,10 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // the read latency after each barrier.
     Regs r0;
     Frags F0, F1;
-    load_stage(r0, 0, 0);
+    load_stage(r0, kofs, 0);
     store_stage(r0, 0);
     __syncthreads();
-    if (nk > 1) load_stage(r0, BK6B, 1);
+    if (nk > 1) load_stage(r0, kofs + BK6B, 1);
     read_frags(F0, 0, 0);
     mfmas(F0);
     read_frags(F1, 0, 1);
@@ -1002,7 +1022,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     __syncthreads();
     for (int kc = 1; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B, buf ^ 1);
+        if (kc + 1 < nk) load_stage(r0, kofs + (kc + 1) * BK6B, buf ^ 1);
         read_frags(F0, buf, 0);
         __builtin_amdgcn_sched_barrier(0);  // issue the reads before the MFMAs that hide them
         mfmas(F1);
@@ -1023,12 +1043,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
     // time to land.
     Regs r0, r1;
-    load_stage(r0, 0, 0);
+    load_stage(r0, kofs, 0);
     store_stage(r0, 0);
-    if (nk > 1) load_stage(r1, BK6B, 1);
+    if (nk > 1) load_stage(r1, kofs + BK6B, 1);
     __syncthreads();
     auto step = [&](int kc, Regs& hold, Regs& next) {
-        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6B, kc & 1);  // (no LDS-DMA with two register stages)
+        if (kc + 2 < nk) load_stage(next, kofs + (kc + 2) * BK6B, kc & 1);  // (no LDS-DMA with two register stages)
         compute(kc & 1);
         if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
         __syncthreads();
@@ -1039,12 +1059,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     }
 #else
     Regs r0;
-    load_stage(r0, 0, 0);
+    load_stage(r0, kofs, 0);
     store_stage(r0, 0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, (kc + 1) * BK6B, buf ^ 1);
+        if (kc + 1 < nk) load_stage(r0, kofs + (kc + 1) * BK6B, buf ^ 1);
         compute(buf);
         if (kc + 1 < nk) store_stage(r0, buf ^ 1);
         __syncthreads();
@@ -1092,7 +1112,10 @@ static bool x6b_presplit(const ConvParams& p) {
 static int launch_x6b(const ConvParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
     EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
-    const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128);
+    if (p.ksplit > 1)
+        EDGEDET_REQUIRE(p.ksplit == 2 && !p.res && p.act == 0 && p.Kpad >= 2 * BK6B,
+                        "conv split-K: 2 halves, no residual, no activation (y must be zeroed)");
+    const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128) * (p.ksplit > 1 ? 2 : 1);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
     const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
     if (x6b_presplit(p)) {
@@ -1247,6 +1270,11 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 23: return launch_x6<2, 2, 2, 2>(p, s);  // 128 x 128, bf16x6
         case 24: return launch_x6<4, 2, 2, 2>(p, s);  // 256 x 128, bf16x6
         case 25: return launch_x6b(p, s);             // 256 x 128, bf16x6, 32-deep swizzled stages
+        case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
+            ConvParams q = p;
+            q.ksplit = 2;
+            return launch_x6b(q, s);
+        }
         case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
         case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
         case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128

@@ -27,6 +27,9 @@ MBCONV_FUSE = os.environ.get("EDGEDET_MBCONV_FUSE", "0") == "1"
 # SSDLite features.0.0 + features.0.1 as one kernel (csrc/layers.hip ssd_stem_kernel); =0 lowers the
 # three separate ops.
 SSD_STEM_FUSE = os.environ.get("EDGEDET_SSD_STEM_FUSE", "1") == "1"
+# ResNet bottleneck conv2 without its ReLU (applied by conv3's input load) where split-K pays;
+# EDGEDET_SPLITK_DEFER=0 keeps the ReLU in conv2.
+SPLITK_DEFER = os.environ.get("EDGEDET_SPLITK_DEFER", "1") == "1"
 
 
 def _np(t):
@@ -537,12 +540,16 @@ class FasterRCNNFPNv2(_Detector):
                 q = f"{p}{lname}.{bi}."
                 s = stride if bi == 0 else 1
                 y = conv(cur, q + "conv1.weight", q + "bn1", 1, 1, "RE")
-                y = conv(y, q + "conv2.weight", q + "bn2", 3, s, "RE")
+                # deep-K 3x3 convs on small maps (layer3/4 at detection batch sizes) fill the GPU only
+                # with split-K (tile 26), which cannot apply the ReLU: conv3 applies it to its input
+                m = y[1][0] * ((y[1][1] - 1) // s + 1) * ((y[1][2] - 1) // s + 1)  # output pixels
+                defer = SPLITK_DEFER and 9 * width >= 2048 and -(-m // 256) * -(-width // 128) < 200
+                y = conv(y, q + "conv2.weight", q + "bn2", 3, s, None if defer else "RE")
                 if bi == 0:
                     idn = conv(cur, q + "downsample.0.weight", q + "downsample.1", 1, s, None)
                 else:
                     idn = cur
-                cur = conv(y, q + "conv3.weight", q + "bn3", 1, 1, "RE", res=idn[0])
+                cur = conv(y, q + "conv3.weight", q + "bn3", 1, 1, "RE", res=idn[0], in_relu=defer)
             cs.append(cur)
 
         return inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs

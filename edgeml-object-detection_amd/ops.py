@@ -189,7 +189,8 @@ def conv2d_nhwc(x, w_packed, bias, cout, k, stride, pad, act=None, res=None, til
     B, H, W, Cin = x.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
-    y = torch.empty((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
+    # tile 26 (split-K) accumulates into y: it must start zeroed
+    y = (torch.zeros if tile == 26 else torch.empty)((B, Ho, Wo, cout), dtype=torch.float32, device=x.device)
     x3 = torch.empty(3 * B * H * W * Cin + 32, dtype=torch.int16, device=x.device) if presplit else None
     if tile == 0 and in_scale is None:
         if x3 is not None:

@@ -348,6 +348,14 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
         t = CONV_TILES.get(conv_key(op))
         if t and (w3 is not None or t < 20):
             op.i[23] = int(t)
+    if op.i[23] == 26:
+        # split-K accumulates into y: only for a dense output without activation or residual, zeroed
+        # by a MEMSET record right before the conv (another conv of the same shape key may not qualify)
+        dense = yp == cout and y_off == 0 and (y_bstride is None or y_bstride == Ho * Wo * cout)
+        if act is None and res is None and dense and w3 is not None:
+            plan.add(Op(ops.MEMSET, {0: B * Ho * Wo * cout * 4}, {0: y}, name=name + ".zero"))
+        else:
+            op.i[23] = 25
     # only where an input transform is fused: the split pass then also takes the per-element GN / SE
     # arithmetic out of the GEMM loop (measured: GN+ReLU head conv 1.83 -> 1.74 ms); for a plain input
     # the extra pass costs more than the in-loop split (box head 2.48 -> 2.60 ms)

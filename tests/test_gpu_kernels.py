@@ -307,6 +307,24 @@ def test_conv_bf16x6_presplit_bit_identical(case, se):
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[6], CONV_CASES[7], (2, 20, 20, 672, 546, 1, 1, None, False),
+                                  (3, 10, 10, 480, 546, 1, 1, None, False), (1, 9, 9, 64, 64, 3, 1, None, False)])
+def test_conv_bf16x6_split_k(case):
+    """Tile 26: the 256 x 128 bf16x6 tile with K in two halves added into a zeroed output (the first
+    half adds the bias).  Matches torch, and two runs are bit-identical (a + b == b + a)."""
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight
+    _conv_case(*case, tile=26, x6=True)
+    B, H, W, Cin, Cout, k, s, act, res = case
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(B, H, W, Cin, generator=g).to(DEV)
+    wp = torch.from_numpy(pack_conv_weight(torch.randn(Cout, Cin, k, k, generator=g).numpy())[0]).to(DEV)
+    w3 = ops.split_bf16x3(wp)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    y1, y2 = (ops.conv2d_nhwc(x, wp, b, Cout, k, s, (k - 1) // 2, None, tile=26, w3=w3) for _ in range(2))
+    assert torch.equal(y1, y2)
+
+
 @pytest.mark.parametrize("tile", [22, 23, 24, 25])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)

@@ -21,6 +21,7 @@ SHAPES = {  # name: (B, H, W, Cin, Cout, k, stride)
     "ssd_f13": (16, 20, 20, 112, 672, 1, 1),
     "ssd_12_3": (16, 20, 20, 672, 112, 1, 1),
     "retina_cls": (8, 100, 100, 256, 819, 3, 1),
+    "ssd_head_cls1b": (16, 10, 10, 480, 546, 1, 1),
 }
 
 
@@ -48,7 +49,7 @@ def main():
         for tv in a.tiles.split(","):  # "25p": tile 25 with the input pre-split (x3 scratch)
             t, ps = int(tv.rstrip("p")), tv.endswith("p")
             for use3 in ((False, True) if t == 0 else (t >= 20,)):
-                f = lambda: ops.conv2d_nhwc(x, wp, b, Cout, k, s, pad, "RE", tile=t, w3=w3 if use3 else None,
+                f = lambda: ops.conv2d_nhwc(x, wp, b, Cout, k, s, pad, None if t == 26 else "RE", tile=t, w3=w3 if use3 else None,
                                             presplit=ps)
                 f()
                 torch.cuda.synchronize()
