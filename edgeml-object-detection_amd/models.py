@@ -220,10 +220,14 @@ class SSDLite320(_Detector):
         small, so two chains overlap one chain's latency-bound tail (NMS) and small kernels with the
         other's work.  EDGEDET_SSD_CHAINS overrides (1 = one chain)."""
         n = int(os.environ.get("EDGEDET_SSD_CHAINS", "0")) or self.CHAINS
-        n = max(1, min(n, ops.MAX_LANES, B // 8 if B >= 16 else 1))
-        while B % n:
-            n -= 1
-        return n
+        return max(1, min(n, ops.MAX_LANES, B // 8 if B >= 16 else 1))
+
+    @staticmethod
+    def chain_split(B, n):
+        """(first image, images) of each chain: B split as evenly as possible (earlier chains +1)."""
+        q, r = divmod(B, n)
+        starts = [c * q + min(c, r) for c in range(n)]
+        return [(b0, q + (1 if c < r else 0)) for c, b0 in enumerate(starts)]
 
     def build_plan(self, B, H, W, pack_only=False):
         P = Plan(self.pack, self.device or "cpu")
@@ -232,10 +236,10 @@ class SSDLite320(_Detector):
         shared = {}
         if nch > 1:
             P.fork(nch - 1)
-        for c in range(nch):
+        for c, (b0, bc) in enumerate(self.chain_split(B, nch)):
             if nch > 1:
                 P.lane(c)
-            self._lower_chain(P, c, B // nch, B, H, W, inp, shared, nch, pack_only)
+            self._lower_chain(P, c, b0, bc, B, H, W, inp, shared, nch, pack_only)
             if pack_only:
                 return P
         if nch > 1:
@@ -248,12 +252,12 @@ class SSDLite320(_Detector):
         P.chains = nch
         return P
 
-    def _lower_chain(self, P, c, B, Btot, H, W, inp, shared, nch, pack_only):
-        """Lower the forward of images [c*B, (c+1)*B) (B per chain, Btot in the plan)."""
+    def _lower_chain(self, P, c, img0, B, Btot, H, W, inp, shared, nch, pack_only):
+        """Lower the forward of images [img0, img0 + B) (B in this chain, Btot in the plan)."""
         NC = self.num_classes
         S = self.SIZE
         sfx = f"#{c}" if nch > 1 else ""
-        view = (lambda buf: BufView(buf, c * B, B)) if nch > 1 else (lambda buf: buf)
+        view = (lambda buf: BufView(buf, img0, B)) if nch > 1 else (lambda buf: buf)
         x = P.buf((B, S, S, 4), name="pre" + sfx)
         P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {0: view(inp), 1: x},
                  {0: 0.5, 1: 0.5, 2: 0.5, 3: 0.5, 4: 0.5, 5: 0.5}, name="transform"))
@@ -391,7 +395,7 @@ class SSDLite320(_Detector):
                 w, b, K, Kpad, cin = self._conv_bias(p + ".1.weight", p + ".1.bias")
                 cout = 6 * cols
                 conv_op(P, t[0], t[1], w, b, cout, 1, 1, 0, None, out, (B, fs[1], fs[2], cout), K, Kpad,
-                        y_pstride=cout, y_bstride=A * cols, y_off=c * B * A * cols + off * cols, name=p + ".1" + sfx)
+                        y_pstride=cout, y_bstride=A * cols, y_off=img0 * A * cols + off * cols, name=p + ".1" + sfx)
             off += fs[1] * fs[2] * 6
         if nch == 1:
             P.join()

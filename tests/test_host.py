@@ -278,3 +278,12 @@ def test_estimator_host_helpers_follow_the_reference():
     w = spec.unpack(s)["linear_stacks.0.0.weight"]
     assert np.abs(w).max() <= np.sqrt(6 / 145) and np.abs(w).max() > 0.9 * np.sqrt(6 / 145)
     assert (spec.unpack(s)["linear_stacks.0.1.running_var"] == 1).all()
+
+
+def test_ssd_chain_split_covers_the_batch():
+    from edgeml_amd import models
+    for B, n in [(32, 2), (33, 2), (10, 3), (8, 1), (40, 4)]:
+        parts = models.SSDLite320.chain_split(B, n)
+        assert len(parts) == n and sum(c for _, c in parts) == B
+        assert [b0 for b0, _ in parts] == [sum(c for _, c in parts[:k]) for k in range(n)]
+        assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
