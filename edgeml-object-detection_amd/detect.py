@@ -6,9 +6,10 @@
 Behaviour kept from the reference (detect.py:62-106): images are taken in sorted(os.listdir) order,
 read as RGB and scaled by 1/255, every image gets one ``<name[:-4]>.npy`` (N,6) float64 file
 ``[cls, xc, yc, w, h, conf]`` normalised by the original size, rows in score order, an empty result
-still writes a (0,6) file.  Differences: images of equal size are batched (results are per image and
-identical to batch=1), and under ``torchrun`` the sorted list is split into contiguous shards, one
-per GPU, with the output rows gathered to rank 0 over RCCL (distributed.py).
+still writes a (0,6) file.  Differences: images of equal size are batched across the whole list
+(results are per image and identical to batch=1) and decoded by a thread pool ahead of the engine,
+and under ``torchrun`` the sorted list is split into contiguous shards, one per GPU, with the output
+rows gathered to rank 0 over RCCL (distributed.py).
 """
 import argparse
 import os
@@ -68,6 +69,34 @@ class ObjectDetectionDataset:
         return image / 255
 
 
+def _image_size(path):
+    from PIL import Image
+    with Image.open(path) as im:  # header only
+        return im.size[1], im.size[0]
+
+
+def _decoded_batches(dataset, batch, workers=None):
+    """Yield (names, [3,H,W] float images) for batches of at most `batch` equal-size images: groups
+    by size in first-appearance order, names in sorted order within a group.  Decoding runs on a
+    thread pool with the next batch in flight while the caller uses the current one."""
+    import concurrent.futures as cf
+    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
+    with cf.ThreadPoolExecutor(workers) as ex:
+        sizes = list(ex.map(_image_size, paths))
+        groups = {}
+        for i, hw in enumerate(sizes):
+            groups.setdefault(hw, []).append(i)
+        chunks = [idx[k:k + batch] for idx in groups.values() for k in range(0, len(idx), batch)]
+        fut = [ex.submit(lambda c=c: [dataset[i] for i in c]) for c in chunks[:2]]
+        for j, c in enumerate(chunks):
+            imgs = fut[j].result()
+            if j + 2 < len(chunks):
+                fut.append(ex.submit(lambda c=chunks[j + 2]: [dataset[i] for i in c]))
+            fut[j] = None
+            yield [dataset.img_names[i] for i in c], imgs
+
+
 def detect_rows(model, images, dataset="coco"):
     """Run the engine on a list of [3,H,W] float images; return the .npy rows per image."""
     preds = model(images)
@@ -97,21 +126,11 @@ def main(opts):
     Path(opts.save_dir).mkdir(parents=True, exist_ok=True)
     batch = getattr(opts, "batch", None) or model.max_batch
     results = {}
-    pending = []
-
-    def flush():
-        imgs = [im for _, im in pending]
-        for (name, _), r in zip(pending, detect_rows(model, imgs, opts.dataset)):
+    # Batches of equal-size images across the whole shard (sizes from the file headers, no decode),
+    # decoded by a thread pool one batch ahead of the engine (PIL releases the GIL while decoding).
+    for names, imgs in _decoded_batches(dataset, batch):
+        for name, r in zip(names, detect_rows(model, imgs, opts.dataset)):
             results[name] = r
-        pending.clear()
-
-    for i in range(len(dataset)):
-        img = dataset[i]
-        if pending and (tuple(pending[-1][1].shape) != tuple(img.shape) or len(pending) >= batch):
-            flush()
-        pending.append((my_names[i], img))
-    if pending:
-        flush()
     if world > 1:
         results = dist_mod.gather_rows(results, my_names, img_names, rank, world)
     if rank == 0:

@@ -143,6 +143,15 @@ def pack_dw_weight(w_c1kk):
 
 
 # ------------------------------------------------------------------------------ arena + ops
+_ESIZE = {}
+
+
+def _esize(dtype):
+    if dtype not in _ESIZE:
+        _ESIZE[dtype] = torch.empty(0, dtype=dtype).element_size()
+    return _ESIZE[dtype]
+
+
 class Buf:
     """A carve-out of the plan arena (float32 unless dtype says otherwise)."""
 
@@ -150,7 +159,7 @@ class Buf:
         self.shape = tuple(int(s) for s in shape)
         self.dtype = dtype
         self.name = name
-        self.nbytes = int(np.prod(self.shape)) * torch.tensor([], dtype=dtype).element_size()
+        self.nbytes = int(np.prod(self.shape)) * _esize(dtype)
         self.off = None
         self.plan = None
 
@@ -159,7 +168,7 @@ class Buf:
 
     def tensor(self):
         n = int(np.prod(self.shape))
-        es = torch.tensor([], dtype=self.dtype).element_size()
+        es = _esize(self.dtype)
         flat = self.plan.arena[self.off:self.off + n * es].view(self.dtype)
         return flat.view(self.shape)
 
