@@ -556,8 +556,10 @@ template <int NT, int KC>
 __device__ void nms_block(SegSmem<KC>& S, int m, const IouThr& thr, bool groups) {
     constexpr int NWORDS = KC / 64;
     const int nw = (m + 63) >> 6;
+    // row i varies fastest across lanes: a wave's lanes read the same S.box[j] (an LDS broadcast)
+    // while their own rows are consecutive (w-fastest put 16 lanes on one bank, 1 KiB apart)
     for (int t = threadIdx.x; t < m * nw; t += NT) {
-        const int i = t / nw, w = t - (t / nw) * nw;
+        const int w = t / m, i = t - w * m;
         unsigned long long bits = 0ull;
         if (w >= (i >> 6)) {
             const f32x4 bi = S.box[i];
@@ -1124,10 +1126,19 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
         k = float_key(ob[i]);
         return true;
     };
+#ifdef RPN_PROFILE
+    long long tp = __builtin_amdgcn_s_memtime(), t_sel = 0, t_cmp = 0, t_sort = 0, t_dec = 0, t_nms = 0;
+#define RPN_STAMP(acc) do { __syncthreads(); const long long tn = __builtin_amdgcn_s_memtime(); acc += tn - tp; tp = tn; } while (0)
+#else
+#define RPN_STAMP(acc) do { } while (0)
+#endif
     const uint32_t T = radix_select<NT>(L.n, P.topk, fkey, S.hist, S.misc);
+    RPN_STAMP(t_sel);
     const bool take_all = S.misc[1] <= P.topk;
     const int m = compact<NT>(L.n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    RPN_STAMP(t_cmp);
     bitonic_desc<NT>(S.keys, nullptr, m);
+    RPN_STAMP(t_sort);
     for (int t = threadIdx.x; t < m; t += NT) {
         const int i = key_index(S.keys[t]);
         const f32x4 d = db[i];
@@ -1139,7 +1150,14 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
         S.valid[t] = ((bx.z - bx.x) >= P.min_size && (bx.w - bx.y) >= P.min_size && score >= P.score_thresh) ? 1 : 0;
     }
     __syncthreads();
+    RPN_STAMP(t_dec);
     nms_block<NT, KC>(S, m, P.iou, false);
+    RPN_STAMP(t_nms);
+#ifdef RPN_PROFILE
+    if (threadIdx.x == 0 && b == 0)
+        printf("rpn level %d n %d: select %lld compact %lld sort %lld decode %lld nms %lld\n", l, L.n, t_sel, t_cmp,
+               t_sort, t_dec, t_nms);
+#endif
     write_kept<NT, KC>(S, m, b * P.nlevels + l, out, [&](int t, int64_t o) {
         const float logit = key_float((uint32_t)(S.keys[t] >> 32));
         out.box[o] = S.box[t];
