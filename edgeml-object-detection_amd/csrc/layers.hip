@@ -912,14 +912,15 @@ __host__ __device__ inline void bilinear_setup(float y, float x, int H, int W, i
 
 // One output element group (4 channels of one bin of one RoI).  __host__ __device__ so the exact
 // kernel body also runs in the host-side debug harness (tools/roi_align_host_check.cpp, ASan).
-__host__ __device__ inline void roi_align_thread(const RoiParams& p, int64_t idx) {
+__host__ __device__ inline void roi_align_thread(const RoiParams& p, int r, int j) {
+    // j = (ph * PW + pw) * C4 + c/4 within RoI r: 32-bit index math (int64 division is a long
+    // software sequence on the GPU and used to dominate the kernel)
     const int C4 = p.C >> 2;
-    const int c = (int)(idx % C4) * 4;
-    int64_t t = idx / C4;
-    const int pw = (int)(t % p.PW);
-    t /= p.PW;
-    const int ph = (int)(t % p.PH);
-    const int r = (int)(t / p.PH);
+    const int bin = j / C4;
+    const int c = (j - bin * C4) * 4;
+    const int ph = bin / p.PW;
+    const int pw = bin - ph * p.PW;
+    const int64_t idx = (int64_t)r * (p.PH * p.PW * C4) + j;
     float* o = p.out + idx * 4;
     int b, lvl = 0;
     float x1, y1, x2, y2;
@@ -984,11 +985,12 @@ __host__ __device__ inline void roi_align_thread(const RoiParams& p, int64_t idx
     *reinterpret_cast<f32x4*>(o) = f32x4{acc.x / count, acc.y / count, acc.z / count, acc.w / count};
 }
 
-__global__ void roi_align_kernel(RoiParams p) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)p.R * p.PH * p.PW * (p.C >> 2);
-    if (idx >= total) return;
-    roi_align_thread(p, idx);
+// grid (R, bins x channel groups of one RoI / 256): the RoI, its level and sampling grid are
+// uniform across the workgroup
+__global__ void __launch_bounds__(256) roi_align_kernel(RoiParams p) {
+    const int j = blockIdx.y * 256 + threadIdx.x;
+    if (j >= p.PH * p.PW * (p.C >> 2)) return;
+    roi_align_thread(p, blockIdx.x, j);
 }
 
 int roi_align_launch(const RoiParams& p, hipStream_t s) {
@@ -998,7 +1000,9 @@ int roi_align_launch(const RoiParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.nlevels >= 1 && p.nlevels <= 4, "roi_align: 1..4 levels");
     const int64_t total = (int64_t)p.R * p.PH * p.PW * (p.C / 4);
     if (total == 0) return 0;
-    hipLaunchKernelGGL(roi_align_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    EDGEDET_REQUIRE((int64_t)p.PH * p.PW * (p.C / 4) <= 65535 * 256, "roi_align: too many bins x channels");
+    hipLaunchKernelGGL(roi_align_kernel, dim3((unsigned)p.R, (unsigned)cdiv(p.PH * p.PW * (p.C / 4), 256)), dim3(256),
+                       0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

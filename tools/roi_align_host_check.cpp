@@ -22,7 +22,7 @@ int main(int argc, char** argv) {
     p.rois = rois.data(); p.mode = 0; p.R = R; p.B = B; p.C = C; p.PH = 7; p.PW = 7; p.sr = 2;
     p.out = out.data();
     const int64_t total = (int64_t)R * 49 * (C / 4);
-    for (int64_t i = 0; i < total; ++i) roi_align_thread(p, i);
+    for (int64_t i = 0; i < total; ++i) roi_align_thread(p, (int)(i / (total / p.R)), (int)(i % (total / p.R)));
     double s = 0; for (float v : out) s += v;
     printf("ok sum=%f\n", s);
     return 0;
