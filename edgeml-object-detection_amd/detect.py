@@ -128,9 +128,14 @@ def main(opts):
     results = {}
     # Batches of equal-size images across the whole shard (sizes from the file headers, no decode),
     # decoded by a thread pool one batch ahead of the engine (PIL releases the GIL while decoding).
-    for names, imgs in _decoded_batches(dataset, batch):
-        for name, r in zip(names, detect_rows(model, imgs, opts.dataset)):
-            results[name] = r
+    # Up to model.INFLIGHT batches on the device at once (run_batches), so one batch's NMS tail
+    # overlaps the next batch's backbone.
+    sized = ((names, [(int(im.shape[-2]), int(im.shape[-1])) for im in imgs], imgs)
+             for names, imgs in _decoded_batches(dataset, batch))
+    tagged = (((names, hw), imgs) for names, hw, imgs in sized)
+    for (names, hw), dets in model.run_batches(tagged):
+        for name, (h, w), (b, s, l) in zip(names, hw, dets):
+            results[name] = fmt.format_detections(b, s, l, h, w, opts.dataset)
     if world > 1:
         results = dist_mod.gather_rows(results, my_names, img_names, rank, world)
     if rank == 0:

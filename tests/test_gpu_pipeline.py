@@ -126,3 +126,32 @@ def test_detect_then_reward_cli_equals_oracle_pipeline():
         print("ORIE engine+GPU reward", got, "oracle", ref)
         assert np.any(ref != 0)
         np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("kind", ["ssd", "frcnn"])
+def test_run_batches_matches_call(kind):
+    """model.run_batches (the CLI's path: two batches in flight, each on its own plan instance and
+    stream) gives bit-identical detections to model(images) batch by batch, across a shape change,
+    a ragged last batch and slot reuse."""
+    from edgeml_amd import models, synthetic
+    if kind == "ssd":
+        sd = synthetic.synthetic_state_dict("ssd", 91, True, seed=0)
+        model = models.SSDLite320(sd, 91, True).to("cuda:0")
+    else:
+        model = models.fasterrcnn_resnet50_fpn_v2().to("cuda:0")
+    shapes = [(480, 640)] * 3 + [(640, 640)] * 2
+    batches = []
+    for i, (h, w) in enumerate(shapes):
+        n = 1 if i == 2 else 2
+        imgs = synthetic.make_batch(n, h, w, seed=40 + i)
+        batches.append((i, list(imgs)))
+    got = list(model.run_batches(batches, inflight=2))
+    assert [t for t, _ in got] == list(range(len(batches)))
+    for (tag, dets), (_, imgs) in zip(got, batches):
+        ref = model(imgs)
+        assert len(dets) == len(imgs)
+        for (b, s, l), r in zip(dets, ref):
+            np.testing.assert_array_equal(b, r["boxes"].cpu().numpy())
+            np.testing.assert_array_equal(s, r["scores"].cpu().numpy())
+            np.testing.assert_array_equal(l, r["labels"].cpu().numpy())
+            assert len(s) > 0
