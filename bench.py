@@ -235,7 +235,11 @@ def roofline_for(plan, stream, step_ms, model=""):
         if name != "lanes":
             fam[name] = fam.get(name, 0.0) + t
     dom = max(fam, key=fam.get)
-    op, t = max(((o, t) for o, t in zip(plan.ops, times) if op_work(o)[0] == dom), key=lambda x: x[1])
+    # the family's largest launch by algorithmic work (first in plan order among equal shapes, so
+    # the choice does not flip between identical layers from run to run and the committed PMC
+    # summary of the same launch applies); its measured time prices it
+    op, t = max(((o, t) for o, t in zip(plan.ops, times) if op_work(o)[0] == dom),
+                key=lambda x: (op_work(x[0])[1], op_work(x[0])[2]))
     name, flops, byts = op_work(op)
     kname, peak_tf = {"dwconv": "dwconv_kernel"}.get(name, name), FP32_MFMA_PEAK_TFS
     k = plan.ops.index(op)
