@@ -287,3 +287,25 @@ def test_ssd_chain_split_covers_the_batch():
         assert len(parts) == n and sum(c for _, c in parts) == B
         assert [b0 for b0, _ in parts] == [sum(c for _, c in parts[:k]) for k in range(n)]
         assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def test_bench_attaches_committed_pmc_traffic():
+    """bench.attach_traffic takes the committed rocprofv3 PMC summary for the roofline launch: the
+    same layer in any batch chain ("#k" copies have one shape and grid), never a different shape."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("_bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    with open(os.path.join(root, "profiles", "pmc_ssd.json")) as f:
+        pmc = json.load(f)
+    base = pmc["launch"].split("#")[0]
+    for k in (0, 1):
+        roof = {"launch": f"{base}#{k}", "grid_wg": pmc["grid_wg"], "traffic": None, "_op_index": 3}
+        bench.attach_traffic(roof, "ssd")
+        assert roof["traffic"] == pmc["hbm_bytes_per_launch"] and "_op_index" not in roof
+    for roof in ({"launch": base + "#0", "grid_wg": pmc["grid_wg"] + 1, "traffic": None},
+                 {"launch": "backbone.features.0.0#0", "grid_wg": pmc["grid_wg"], "traffic": None}):
+        bench.attach_traffic(roof, "ssd")
+        assert roof["traffic"] is None
