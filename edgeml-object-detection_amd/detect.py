@@ -111,20 +111,20 @@ def detect_rows(model, images, dataset="coco"):
 def main(opts):
     from . import distributed as dist_mod
     img_names = sorted(os.listdir(opts.img_dir))
-    rank, world = dist_mod.rank_world()
+    if not torch.cuda.is_available():
+        raise RuntimeError("edgeml_amd.detect needs an MI355X (HIP) device; there is no CPU path")
+    rank, world = dist_mod.ensure_initialized()
     my_names = dist_mod.shard(img_names, rank, world)
     dataset = ObjectDetectionDataset(opts.img_dir, my_names)
     num_class = 91 if opts.dataset == "coco" else 21
-    if not torch.cuda.is_available():
-        raise RuntimeError("edgeml_amd.detect needs an MI355X (HIP) device; there is no CPU path")
-    device = f"cuda:{dist_mod.local_rank()}"
+    device = f"cuda:{dist_mod.device_index()}"
     torch.cuda.set_device(device)
     if rank == 0:
         print(f"Using {device} device (world {world})")
     model = load_weak_models(opts.model, opts.model_path, num_class).to(device)
     model.eval()
     Path(opts.save_dir).mkdir(parents=True, exist_ok=True)
-    batch = getattr(opts, "batch", None) or model.max_batch
+    batch = min(getattr(opts, "batch", None) or model.max_batch, model.max_batch)
     results = {}
     # Batches of equal-size images across the whole shard (sizes from the file headers, no decode),
     # decoded by a thread pool one batch ahead of the engine (PIL releases the GIL while decoding).

@@ -14,6 +14,27 @@ import torch
 import torch.distributed as dist
 
 
+def ensure_initialized():
+    """Join the process group torchrun describes (WORLD_SIZE > 1 in the environment), once.
+
+    Backend: "nccl" (RCCL over xGMI) when a GPU is visible, "gloo" otherwise; EDGEDET_DIST_BACKEND
+    overrides (the multi-process GPU tests run two gloo ranks on one card).  With nccl each rank
+    binds its LOCAL_RANK's device before the group is created.  Returns (rank, world)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and dist.is_available() and not dist.is_initialized():
+        backend = os.environ.get("EDGEDET_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(device_index())
+        dist.init_process_group(backend)
+    return rank_world()
+
+
+def device_index():
+    """This rank's GPU: LOCAL_RANK, wrapped onto the visible devices (ranks may share a card)."""
+    n = torch.cuda.device_count()
+    return local_rank() % n if n else 0
+
+
 def rank_world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()

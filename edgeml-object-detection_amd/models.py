@@ -742,9 +742,12 @@ class FasterRCNNFPNv2(_Detector):
                   7: P.out_score, 8: P.out_label, 9: P.out_count}, name="roi_heads.detections_per_img"))
         P.input = inp
         P.feats = [o[0] for o in outs]
+        P.rpn_heads = heads  # per level (objectness [B,H,W,3], deltas [B,H,W,12]): the parity tests' RPN inputs
         P.proposals, P.proposal_count = props, pcount
         P.box_features = roi
         P.pred = pred
+        P.box_scores, P.box_decoded = scores, bxs
+        P.resized = (Ho, Wo, Hp, Wp)
         return P
 
 
@@ -867,6 +870,8 @@ class RetinaNetFPNv2(FasterRCNNFPNv2):
         P.feats = [o[0] for o in outs]
         P.cls_logits, P.bbox_regression = cls, reg
         P.cand_count = lrec[4]
+        P.level_anchors = na  # anchors per level in the concatenated head outputs (parity tests)
+        P.resized = (Ho, Wo, Hp, Wp)
         return P
 
 

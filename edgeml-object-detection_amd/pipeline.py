@@ -30,12 +30,7 @@ def main(opts):
     from . import distributed as dist_mod
     if not torch.cuda.is_available():
         raise RuntimeError("edgeml_amd.pipeline needs an MI355X (HIP) device; there is no CPU path")
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        import torch.distributed as dist
-        if not dist.is_initialized():
-            torch.cuda.set_device(dist_mod.local_rank())
-            dist.init_process_group("nccl")
-    rank, _ = dist_mod.rank_world()
+    rank, _ = dist_mod.ensure_initialized()
     times = {}
     dirs = {k: os.path.join(opts.work_dir, k) for k in ("weak", "strong", "reward")}
     for stage, model in (("weak", opts.weak), ("strong", opts.strong)):

@@ -210,8 +210,8 @@ def main(opts):
     if not torch.cuda.is_available():
         raise RuntimeError("edgeml_amd.reward needs an MI355X (HIP) device; there is no CPU path")
     from . import distributed as dist_mod
-    rank, world = dist_mod.rank_world()
-    device = f"cuda:{dist_mod.local_rank()}"
+    rank, world = dist_mod.ensure_initialized()
+    device = f"cuda:{dist_mod.device_index()}"
     torch.cuda.set_device(device)
     weak_data, strong_data, labels = set_data(opts.weak_dir, opts.strong_dir, opts.label_dir, device)
     num_img = len(labels)

@@ -74,7 +74,15 @@ def _is_residual_bn(kind, name):
 
 
 def synthetic_state_dict(kind, num_classes=91, reduced_tail=True, seed=0, calibrated=True):
-    """Deterministic torchvision-keyed state_dict for ``kind`` in {"ssd", "faster_rcnn"}."""
+    """Deterministic torchvision-keyed state_dict for ``kind`` in {"ssd", "faster_rcnn", "retinanet"}.
+
+    The committed BN calibration tables were measured on the seed-0 weight draws: with another seed
+    the running statistics do not match the weights and activations grow by orders of magnitude
+    (an ill-conditioned network on which fp32 summation-order noise reaches 1e-2), so calibrated
+    weights exist for seed 0 only."""
+    if calibrated and seed != 0:
+        raise ValueError("calibrated synthetic weights exist for seed=0 only (data/calib_*.npz); "
+                         "pass calibrated=False for other seeds")
     table = table_for(kind, num_classes, reduced_tail)
     g = torch.Generator().manual_seed(seed)
     sd = {}

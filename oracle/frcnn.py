@@ -75,8 +75,9 @@ def fpn(cs, sd, hook=None):
     return res
 
 
-def rpn(feats, sd, image_shapes, padded_size):
-    """RegionProposalNetwork eval (SURVEY A.2 step 4) -> list of [<=1000, 4] proposals."""
+def rpn_head(feats, sd, padded_size):
+    """RPNHead over every level + AnchorGenerator: per level objectness logits
+    [N, H*W*A], deltas [N, H*W*A, 4] in (y, x, a) order, and the level's anchors."""
     p = "rpn.head."
     objs, dels = [], []
     for f in feats:
@@ -88,8 +89,18 @@ def rpn(feats, sd, image_shapes, padded_size):
         objs.append(o.view(N, A, 1, H, W).permute(0, 3, 4, 1, 2).reshape(N, -1))
         dels.append(d.view(N, A, 4, H, W).permute(0, 3, 4, 1, 2).reshape(N, -1, 4))
     anchors = tv_ops.rpn_anchors([f.shape[-2:] for f in feats], padded_size)
+    return objs, dels, anchors
+
+
+def rpn(feats, sd, image_shapes, padded_size):
+    """RegionProposalNetwork eval (SURVEY A.2 step 4) -> list of [<=1000, 4] proposals."""
+    return rpn_filter(*rpn_head(feats, sd, padded_size), image_shapes)
+
+
+def rpn_filter(objs, dels, anchors, image_shapes):
+    """RegionProposalNetwork.filter_proposals over the head outputs of rpn_head."""
     out = []
-    for n in range(feats[0].shape[0]):
+    for n in range(objs[0].shape[0]):
         bl, sl, ll = [], [], []
         for lvl, (o, d, a) in enumerate(zip(objs, dels, anchors)):
             k = min(RPN_PRE_NMS, o.shape[1])
@@ -157,14 +168,25 @@ class FasterRCNNOracle:
         x, sizes = tv_ops.transform(list(images), MEAN, STD, MIN_SIZE, MAX_SIZE, divisible=DIVISIBLE)
         feats = fpn(resnet_body(x, sd, hook), sd, hook)
         props = rpn(feats, sd, sizes, tuple(x.shape[-2:]))
+        logits, deltas = self.box_stage(feats, props, sizes, hook, sd)
+        self.used_keys = sd.used
+        return logits, deltas, props, sizes, feats
+
+    @torch.no_grad()
+    def box_stage(self, feats, props, sizes, hook=None, sd=None):
+        """MultiScaleRoIAlign + box head + predictor over given proposals (a list of [R_i, 4])."""
+        sd = _SD(self.sd) if sd is None else sd
         mh = max(s[0] for s in sizes)
         scales = [2.0 ** round(float(torch.tensor(f.shape[-2] / mh).log2())) for f in feats[:4]]
         roi = tv_ops.multiscale_roi_align(feats[:4], props, scales)
         if hook is not None:
             hook("__roi_features__", roi)
-        logits, deltas = box_head(roi, sd, hook)
-        self.used_keys = sd.used
-        return logits, deltas, props, sizes, feats
+        return box_head(roi, sd, hook)
+
+    @torch.no_grad()
+    def rpn_raw(self, feats, padded_size):
+        """The RPN head outputs and anchors the proposal filter consumes (see rpn_head)."""
+        return rpn_head(feats, _SD(self.sd), padded_size)
 
     @torch.no_grad()
     def __call__(self, images):

@@ -87,3 +87,39 @@ def test_gather_values_world2(n):
     for p in procs:
         p.join(timeout=60)
     assert got == [1.5 * i for i in range(n)]
+
+
+def _init_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), EDGEDET_DIST_BACKEND="gloo")
+    from edgeml_amd import distributed as D
+    r, w = D.ensure_initialized()
+    r2, w2 = D.ensure_initialized()  # idempotent
+    out = D.gather_values(np.asarray([10.0 * r]), [r], world, r, w)
+    if r == 0:
+        q.put((r, w, r2, w2, dist.get_backend(), out.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ensure_initialized_joins_torchrun_group():
+    """The CLIs (detect.main, reward.main, pipeline.main) join the group torchrun's environment
+    describes; gloo when no GPU is visible."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_init_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == (0, 2, 0, 2, "gloo", [0.0, 10.0])
+
+
+def test_ensure_initialized_single_process_is_noop(monkeypatch):
+    from edgeml_amd import distributed as D
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert D.ensure_initialized() == (0, 1)
+    assert not dist.is_initialized()

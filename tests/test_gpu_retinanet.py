@@ -3,14 +3,13 @@
 * GN_STATS + the fused GroupNorm-apply/ReLU A-load of the conv against torch's F.group_norm + conv;
 * the raw head outputs (cls logits, box regression of every level) against the oracle forward;
 * the postprocess kernels on identical head outputs against the oracle's postprocess;
-* the final detections of the whole model (match protocol of tests/parity.py).
+* the final detections of the whole model (decision-replay protocol of tests/parity_models.py).
 """
 import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
 
-from tests.parity import match_report
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -102,21 +101,22 @@ def test_retinanet_raw_heads_match_oracle(retina):
 
 
 def test_retinanet_postprocess_on_identical_heads(retina):
-    """The device postprocess fed the oracle's own head outputs: only sigmoid rounding differs."""
-    from edgeml_amd import synthetic
+    """The device postprocess fed the oracle's own head outputs: the decision replay of those head
+    values (host sigmoid / decode) reproduces the device rows to 1 ulp, with no flip."""
+    from edgeml_amd import ops, synthetic
     from oracle import retinanet as R
+    import ctypes
+    from tests import chains
+    from tests.flips import check_replay_reproduces, replay
     sd, model = retina
     imgs = synthetic.make_batch(2, 640, 640, seed=43)
     o = R.RetinaNetOracle(sd, 91)
     cls_ref, reg_ref, anchors, sizes, _ = o.forward_raw(list(imgs))
-    ref = R.postprocess(cls_ref, reg_ref, anchors, sizes)
     plan = model.plan(2, 640, 640)
     plan.input.tensor().copy_(imgs.to(DEV))
     plan.run()  # fills every buffer; then overwrite the heads and re-run only the postprocess ops
     plan.cls_logits.tensor().copy_(torch.cat(cls_ref, 1).to(DEV))
     plan.bbox_regression.tensor().copy_(torch.cat(reg_ref, 1).to(DEV))
-    from edgeml_amd import ops
-    import ctypes
     tail = plan.records[[k for k, op in enumerate(plan.ops) if op.kind in (ops.RETINA_SELECT, ops.RETINA_CLASS_NMS,
                                                                           ops.MERGE_TOPK)]]
     tail = np.ascontiguousarray(tail)
@@ -124,27 +124,30 @@ def test_retinanet_postprocess_on_identical_heads(retina):
     ops.check(ops.lib().edgedet_plan_run(tail.ctypes.data_as(ctypes.c_void_p), len(tail), ops.stream_handle()))
     torch.cuda.synchronize()
     counts = plan.out_count.tensor().cpu().tolist()
-    ratio_w = 1.0  # 640 -> 800: compare in resized pixels (undo the rescale below)
+    scale = np.float32(640) / np.float32(800)
     for j in range(2):
         n = counts[j]
-        got = {"boxes": plan.out_box.tensor()[j, :n].cpu(), "scores": plan.out_score.tensor()[j, :n].cpu(),
-               "labels": plan.out_label.tensor()[j, :n].cpu()}
-        got["boxes"] = got["boxes"] * (800.0 / 640.0) * ratio_w
-        rep = match_report(ref[j], got)
-        print("retinanet postprocess", rep)
-        assert rep["n_ref"] > 0 and rep["scores_sorted"]
-        assert rep["match_frac"] >= 0.99 and rep["max_box_rel"] <= 1e-3
+        sA, _, label_of = chains.retina_sides([c[j] for c in cls_ref], [r[j] for r in reg_ref],
+                                              [c[j] for c in cls_ref], [r[j] for r in reg_ref], anchors, sizes[j])
+        tA = replay(sA, chains.RETINA_STAGES)
+        check_replay_reproduces(tA, sA, plan.out_box.tensor()[j, :n].cpu().numpy(),
+                                plan.out_score.tensor()[j, :n].cpu().numpy(),
+                                plan.out_label.tensor()[j, :n].cpu().numpy(), label_of, scale=scale, rtol=2e-6)
+        ref = R.postprocess([c[j:j + 1] for c in cls_ref], [r[j:j + 1] for r in reg_ref], anchors, sizes[j:j + 1])[0]
+        check_replay_reproduces(tA, sA, ref["boxes"].numpy(), ref["scores"].numpy(), ref["labels"].numpy(), label_of)
+        assert n > 0
 
 
-def test_retinanet_detections_match_oracle(retina):
+@pytest.mark.parametrize("h,w,n", [(480, 640, 1), (640, 640, 2)])
+def test_retinanet_detections_match_oracle(retina, h, w, n):
     from edgeml_amd import synthetic
-    from oracle.retinanet import RetinaNetOracle
+    from tests import parity_models as PM
     sd, model = retina
-    imgs = synthetic.make_batch(1, 480, 640, seed=47)
-    ref = RetinaNetOracle(sd, 91)(list(imgs))
-    got = model(imgs.to(DEV))
-    for r, g in zip(ref, got):
-        rep = match_report(r, g)
-        print("retinanet", rep)
-        assert rep["n_ref"] > 0 and rep["scores_sorted"]
-        assert rep["match_frac"] >= 0.97 and rep["max_box_rel"] <= 1e-3
+    imgs = synthetic.make_batch(n, h, w, seed=47 + h)
+    plan = model.plan(n, h, w)
+    plan.input.tensor().copy_(imgs.to(DEV))
+    plan.run()
+    torch.cuda.synchronize()
+    rep = PM.retina_check(plan, sd, 91, imgs, f"retinanet {n}x{h}x{w}")
+    print(rep)
+    assert rep["rows"] > 0
