@@ -4,7 +4,8 @@
 
 A step = one forward of the detector over one batch of synthetic 640x640 images already resident in
 HBM (preprocess -> backbone -> heads -> decode -> NMS -> final top-k), replayed from a captured
-hipGraph.  N=1 workload: SSDLite320-MobileNetV3 at batch 32 (configs[1]); FRCNN-R50-FPN-v2 at
+hipGraph, plus the D2H copy of the batch's detections (counts, boxes, scores, labels) into pinned
+host memory.  N=1 workload: SSDLite320-MobileNetV3 at batch 32 (configs[1]); FRCNN-R50-FPN-v2 at
 batch 8 (configs[2]) is measured beside it and reported under "frcnn".  For N>1 the script is
 launched by torch.distributed.run: one process per GPU, each replays its own batch (weak scaling:
 images are independent, no collective on the data path); the timed region is bracketed by a
@@ -15,6 +16,10 @@ Extra objects on the JSON line:
                 per launch / its average launch time (HIP events on the plan's stream)
   cpu_baseline  the CPU oracle (a restatement of the reference's torchvision CPU path, detect.py's
                 batch=1 loop) timed on a bounded sample on this host, rank 0 only
+  end_to_end    uint8 host images -> detect.py's .npy rows: pinned staging, H2D of the bytes, forward,
+                D2H, row formatting (model.run_batches, the CLI's path; JPEG decode excluded)
+  orie          the metric's "ORIE max-abs-diff vs ref": ORIE of the engine's SSDLite/FRCNN rows (GPU
+                reward) against ORIE of the CPU oracle's rows (oracle consumer) on a small sample
 """
 import argparse
 import json
@@ -45,25 +50,38 @@ def dist_setup(n_gpus):
     return None, 0, 1
 
 
+def d2h_buffers(plan):
+    """Pinned host buffers for one instance's detections (count, boxes, scores, labels)."""
+    return [(t, torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True))
+            for t in (plan.out_count.tensor(), plan.out_box.tensor(), plan.out_score.tensor(),
+                      plan.out_label.tensor())]
+
+
+def step(plan, stream, d2h):
+    plan.replay(stream)
+    with torch.cuda.stream(stream):
+        for dev, host in d2h:
+            host.copy_(dev, non_blocking=True)
+
+
 def timed_steps(plan, stream, steps, warmup, dist, extra=()):
-    """Time `steps` whole-batch passes. With `extra` = [(plan, stream), ...] the passes rotate over
-    independent plan instances (own arena, own graph) on their own streams, so batch k+1's first
-    convolutions overlap batch k's low-occupancy NMS tail; every pass is still a complete forward
-    of its own batch, and each instance's passes stay ordered on its stream."""
-    lanes = [(plan, stream)] + list(extra)
+    """Time `steps` whole-batch passes (forward graph + D2H of the detections). With `extra` =
+    [(plan, stream), ...] the passes rotate over independent plan instances (own arena, own graph,
+    own pinned output buffers) on their own streams, so batch k+1's first convolutions overlap batch
+    k's low-occupancy NMS tail; every pass is still a complete forward of its own batch, and each
+    instance's passes stay ordered on its stream."""
+    lanes = [(p, s, d2h_buffers(p)) for p, s in [(plan, stream)] + list(extra)]
     for i in range(warmup):
-        p, s = lanes[i % len(lanes)]
-        p.replay(s)
-    for _, s in lanes:
+        step(*lanes[i % len(lanes)])
+    for _, s, _ in lanes:
         s.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        p, s = lanes[i % len(lanes)]
-        p.replay(s)
-    for _, s in lanes:
+        step(*lanes[i % len(lanes)])
+    for _, s, _ in lanes:
         s.synchronize()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -73,6 +91,27 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
+
+
+def end_to_end(m, B, batches, seed):
+    """uint8 host images -> the .npy rows detect.py writes, through model.run_batches as the detect
+    CLI runs it: each batch is a pinned uint8 [B,3,640,640] buffer (the CLI's decode pool writes the
+    decoded images straight into one), uploaded as bytes, /255 on the device, forward, D2H of the
+    detections, rows by fmt.format_batch (byte-identical to detect.py:79-103), two batches in flight.
+    JPEG decode is excluded (the CLI's thread pool; tools/pipeline_bench.py times it)."""
+    from edgeml_amd import fmt, synthetic
+    imgs = synthetic.make_batch_u8(B, 640, 640, seed=seed).pin_memory()
+    work = [(k, imgs) for k in range(batches)]
+    for _ in m.run_batches(work[:2], raw=True):
+        pass
+    torch.cuda.synchronize()
+    n, t0 = 0, time.perf_counter()
+    for _, cnt, box, score, label in m.run_batches(work, raw=True):
+        n += len(fmt.format_batch(box, score, label, cnt, 640, 640))
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 2), "unit": "images/s", "images": n, "batch": B,
+            "path": "pinned uint8 host images -> H2D (bytes) -> forward -> D2H -> .npy rows "
+                    "(no JPEG decode, no file write)"}
 
 
 def inflight_instances(m, B, n, seed):
@@ -288,12 +327,64 @@ def attach_traffic(roof, model):
 
 
 # ------------------------------------------------------------------------------ CPU baseline
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def orie_vs_ref(n=6, E=5):
+    """ORIE of the engine's files vs ORIE of the CPU oracle's files on n synthetic images (SSDLite
+    weak, FRCNN strong; pseudo ground truth = the oracle strong detector's confident boxes): the
+    engine side goes through the product consumer (GPU reward), the reference side through the
+    oracle consumer (oracle/orie.py, pinned to the reference's own G2 values)."""
+    import tempfile
+    import warnings
+    from edgeml_amd import fmt, models, reward, synthetic
+    from oracle import orie
+    from oracle.frcnn import FasterRCNNOracle
+    from oracle.ssdlite import SSDLiteOracle
+    warnings.filterwarnings("ignore")
+    sd_w, sd_s = synthetic.synthetic_state_dict("ssd", 91, True), synthetic.synthetic_state_dict("faster_rcnn", 91)
+    eng = {"weak": models.SSDLite320(sd_w, 91, True).to("cuda"), "strong": models.FasterRCNNFPNv2(sd_s, 91).to("cuda")}
+    ref = {"weak": SSDLiteOracle(sd_w, 91, True), "strong": FasterRCNNOracle(sd_s, 91)}
+    with tempfile.TemporaryDirectory() as td:
+        d = lambda *p: os.path.join(td, *p)  # noqa: E731
+        for sub in ("eng_weak", "eng_strong", "ref_weak", "ref_strong", "labels"):
+            os.makedirs(d(sub))
+        for i in range(n):
+            img = synthetic.make_batch(1, 640, 640, seed=7000 + i)
+            name = f"{i:012d}.png"
+            for tag in ("weak", "strong"):
+                p = eng[tag](img.cuda())[0]
+                fmt.save_npy(d("eng_" + tag), name, fmt.format_detections(
+                    p["boxes"].cpu().numpy(), p["scores"].cpu().numpy(), p["labels"].cpu().numpy(), 640, 640))
+                q = ref[tag]([img[0]])[0]
+                rows = fmt.format_detections(q["boxes"].numpy(), q["scores"].numpy(), q["labels"].numpy(), 640, 640)
+                fmt.save_npy(d("ref_" + tag), name, rows)
+                if tag == "strong":
+                    with open(d("labels", name[:-4] + ".txt"), "w") as f:
+                        for r in rows[rows[:, 5] >= 0.3]:
+                            f.write(" ".join([str(int(r[0]))] + [repr(float(v)) for v in r[1:5]]) + "\n")
+        wd, sd, lab = reward.set_data(d("eng_weak"), d("eng_strong"), d("labels"))
+        got = reward.compute_orie_all(wd, sd, lab, E, seed=1000)
+        want = orie.orie_all(d("ref_weak"), d("ref_strong"), d("labels"), E, seed=1000)
+    return {"max_abs_diff": float(np.abs(got - want).max()), "images": n, "num_ensemble": E,
+            "nonzero_ref": int(np.count_nonzero(want))}
+
+
 def cpu_baseline(kind, budget_s=15.0):
     """The CPU oracle (restated reference path) on a bounded sample, batch=1 like detect.py."""
     from edgeml_amd import synthetic
     from oracle.frcnn import FasterRCNNOracle
     from oracle.ssdlite import SSDLiteOracle
-    torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    from edgeml_amd.distributed import usable_cpus
+    torch.set_num_threads(usable_cpus())
     if kind == "ssd":
         m = SSDLiteOracle(synthetic.synthetic_state_dict("ssd", 91, True), 91, True)
     else:
@@ -308,6 +399,7 @@ def cpu_baseline(kind, budget_s=15.0):
         if el >= budget_s or n >= 200:
             break
     return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "host_cores": os.cpu_count(), "host_cpu": _cpu_model(),
             "sample": f"{n} synthetic 640x640 images, batch=1 ({el:.1f}s), {kind} CPU oracle "
                       f"(PyTorch-CPU + C restatement of the torchvision eval path)"}
 
@@ -315,8 +407,8 @@ def cpu_baseline(kind, budget_s=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="both", choices=["ssd", "frcnn", "retinanet", "both", "all"])
     ap.add_argument("--retina-batch", type=int, default=8)
     ap.add_argument("--ssd-batch", type=int, default=32)
@@ -327,6 +419,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dump-ops", default="", help="write the per-op device times of each model to this JSON")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host uint8 -> rows) rates")
+    ap.add_argument("--e2e-batches", type=int, default=40)
     args = ap.parse_args()
 
     dist, rank, world = dist_setup(args.gpus)
@@ -350,15 +444,19 @@ def main():
             attach_traffic(out["ssd"]["roofline"], "ssd")
         del plan
         m.plans.clear()
+        if rank == 0 and not args.no_e2e:
+            out["ssd"]["end_to_end"] = end_to_end(m, B, args.e2e_batches, 100 * rank)
+            m.plans.clear()
+            m._slots.clear()
     if args.model in ("retinanet", "all"):
         B = args.retina_batch
         m = models.retinanet_resnet50_fpn_v2().to("cuda")
         plan = m.plan(B, 640, 640)
         plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 70).cuda())
         plan.capture(stream)
-        steps = max(1, args.steps // 2)
+        steps = max(2, args.steps // 10)
         extra = inflight_instances(m, B, args.inflight, 100 * rank + 70)
-        el = timed_steps(plan, stream, steps, max(1, args.warmup // 2), dist, extra)
+        el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
         out["retinanet"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
                             "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
@@ -372,9 +470,9 @@ def main():
         plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 50).cuda())
         plan.capture(stream)
         extra = inflight_instances(m, B, args.inflight, 100 * rank + 50)
-        el = timed_steps(plan, stream, max(1, args.steps // 2), max(1, args.warmup // 2), dist, extra)
+        steps = max(2, args.steps // 10)  # FRCNN steps are ~20x SSD's: about a second of timed work
+        el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
-        steps = max(1, args.steps // 2)
         R = float(plan.proposal_count.tensor().float().mean().item())
         gflop = 2 * (151.45e9 + 128.92e6 * R) / 1e9
         out["frcnn"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
@@ -384,6 +482,11 @@ def main():
             out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "frcnn")
             attach_traffic(out["frcnn"]["roofline"], "frcnn")
         del plan
+        m.plans.clear()
+        if rank == 0 and not args.no_e2e:
+            out["frcnn"]["end_to_end"] = end_to_end(m, B, max(4, args.e2e_batches // 4), 100 * rank + 50)
+            m.plans.clear()
+            m._slots.clear()
     if rank == 0 and args.dump_ops:
         with open(args.dump_ops, "w") as f:
             json.dump(OP_DUMP, f, indent=0)
@@ -408,7 +511,10 @@ def main():
     }
     if "frcnn" in out and primary == "ssd":
         f = out["frcnn"]
-        line["frcnn"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items() if k != "roofline"}
+        line["frcnn"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items()
+                         if k not in ("roofline", "end_to_end")}
+        if "end_to_end" in f:
+            line["frcnn"]["end_to_end"] = f["end_to_end"]
         if "roofline" in f:
             line["frcnn"]["roofline"] = f["roofline"]
     if "retinanet" in out and primary != "retinanet":
@@ -417,7 +523,10 @@ def main():
     if "roofline" in p:
         line["roofline"] = p["roofline"]
     line["dets_per_img"] = p.get("dets_per_img")
+    if "end_to_end" in p:
+        line["end_to_end"] = p["end_to_end"]
     if not args.no_cpu:
+        line["orie"] = orie_vs_ref()
         line["cpu_baseline"] = cpu_baseline(primary, args.cpu_budget)
         if "frcnn" in out and primary == "ssd":
             line["frcnn"]["cpu_baseline"] = cpu_baseline("frcnn", args.cpu_budget)

@@ -7,7 +7,7 @@
 //
 // Record layouts (i = int64 fields, p = device pointers, d = doubles, f = floats):
 //   MEMSET         p0 ptr; i0 bytes
-//   PREPROCESS     p0 x[B,3,H,W]; p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
+//   PREPROCESS     p0 x[B,3,H,W] f32 | 0; p2 x[B,3,H,W] u8 | 0 (exactly one); p1 y[B,Hp,Wp,4]; i0..6 B,H,W,Ho,Wo,Hp,Wp; f0..2 mean; f3..5 std
 //   CONV           p0 x; p1 w[Cout][Kpad]; p2 bias; p3 y; p4 res|0; p5 in_scale|0; p6 w3 bf16 planes|0;
 //                  p7 in_shift|0; i24 in_relu; p8 x3 scratch [3][B*H*W*Cin] bf16 | 0 (pre-split input
 //                  planes for the 256 x 128 bf16x6 tile: the split and the input transform run once
@@ -52,6 +52,9 @@
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 #include <mutex>
 #include <string>
+
+#include <map>
+#include <utility>
 
 #include "kernels.hpp"
 
@@ -128,6 +131,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             PreParams p{};
             p.x = P<const float>(o, 0);
             p.y = P<float>(o, 1);
+            p.xu8 = P<const uint8_t>(o, 2);
             p.B = (int)I[0];
             p.H = (int)I[1];
             p.W = (int)I[2];
@@ -363,34 +367,38 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
     }
 }
 
-// Side streams and fork/join events, created once per (thread, device) and reused by every call.
+// Side streams and fork/join events, created once per (thread, device, caller stream) and reused by
+// every call on that stream: two plans in flight on two caller streams (run_batches) get disjoint
+// side lanes, so their lane work overlaps instead of queueing on one shared side stream.
 struct Lanes {
-    int device = -1;
     hipStream_t side[EDGEDET_MAX_LANES] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t join_ev[EDGEDET_MAX_LANES] = {};
 };
-static thread_local Lanes g_lanes;
+static thread_local std::map<std::pair<int, hipStream_t>, Lanes> g_lanes_by_stream;
 
-static int lanes_ready() {
+static Lanes* lanes_for(hipStream_t caller) {
     int dev = 0;
-    EDGEDET_CHECK_HIP(hipGetDevice(&dev));
-    if (g_lanes.device == dev) return 0;
-    g_lanes = Lanes();
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    auto key = std::make_pair(dev, caller);
+    auto it = g_lanes_by_stream.find(key);
+    if (it != g_lanes_by_stream.end()) return &it->second;
+    Lanes L;
     for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
-        EDGEDET_CHECK_HIP(hipStreamCreateWithFlags(&g_lanes.side[l], hipStreamNonBlocking));
-        EDGEDET_CHECK_HIP(hipEventCreateWithFlags(&g_lanes.join_ev[l], hipEventDisableTiming));
+        if (hipStreamCreateWithFlags(&L.side[l], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L.join_ev[l], hipEventDisableTiming) != hipSuccess)
+            return nullptr;
     }
-    EDGEDET_CHECK_HIP(hipEventCreateWithFlags(&g_lanes.fork_ev, hipEventDisableTiming));
-    g_lanes.device = dev;
-    return 0;
+    if (hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return &(g_lanes_by_stream[key] = L);
 }
 
 static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
     bool need_lanes = false;
     for (int64_t k = 0; k < n && !need_lanes; ++k)
         need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
-    if (need_lanes && lanes_ready() != 0) return -2;
+    Lanes* lanes = need_lanes ? lanes_for(s) : nullptr;
+    EDGEDET_REQUIRE(!need_lanes || lanes, "could not create the side lanes (streams / events)");
     int forked = 0;
     for (int64_t k = 0; k < n; ++k) {
         const edgedet_op& o = ops[k];
@@ -398,21 +406,21 @@ static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
         if (o.kind == EDGEDET_OP_FORK) {
             forked = (int)o.i[0];
             EDGEDET_REQUIRE(forked >= 1 && forked < EDGEDET_MAX_LANES, "fork: 1..3 side lanes");
-            EDGEDET_CHECK_HIP(hipEventRecord(g_lanes.fork_ev, s));
-            for (int l = 1; l <= forked; ++l) EDGEDET_CHECK_HIP(hipStreamWaitEvent(g_lanes.side[l], g_lanes.fork_ev, 0));
+            EDGEDET_CHECK_HIP(hipEventRecord(lanes->fork_ev, s));
+            for (int l = 1; l <= forked; ++l) EDGEDET_CHECK_HIP(hipStreamWaitEvent(lanes->side[l], lanes->fork_ev, 0));
         } else if (o.kind == EDGEDET_OP_JOIN) {
             const int nl = (int)o.i[0];
             EDGEDET_REQUIRE(nl >= 1 && nl < EDGEDET_MAX_LANES, "join: 1..3 side lanes");
             for (int l = 1; l <= nl; ++l) {
-                EDGEDET_CHECK_HIP(hipEventRecord(g_lanes.join_ev[l], g_lanes.side[l]));
-                EDGEDET_CHECK_HIP(hipStreamWaitEvent(s, g_lanes.join_ev[l], 0));
+                EDGEDET_CHECK_HIP(hipEventRecord(lanes->join_ev[l], lanes->side[l]));
+                EDGEDET_CHECK_HIP(hipStreamWaitEvent(s, lanes->join_ev[l], 0));
             }
             forked = 0;
         } else {
             const int lane = (int)o.i[EDGEDET_OP_LANE];
             EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
                             "op on a lane that is not forked");
-            rc = run_op(o, lane == 0 ? s : g_lanes.side[lane]);
+            rc = run_op(o, lane == 0 ? s : lanes->side[lane]);
         }
         if (rc != 0) {
             set_error("op " + std::to_string(k) + " (kind " + std::to_string(o.kind) + "): " + g_error);

@@ -29,7 +29,8 @@ struct ConvParams {
 };
 
 struct PreParams {
-    const float* x;  // [B][3][H][W]
+    const float* x;      // [B][3][H][W] float in [0, 1] (the model contract, detect.py:78), or
+    const uint8_t* xu8;  // [B][3][H][W] the decoded uint8 image (detect.py:57); x / 255 on the device
     float* y;        // [B][Hp][Wp][4]
     int B, H, W, Ho, Wo, Hp, Wp;
     float mean[3], stdv[3];

@@ -15,7 +15,17 @@ namespace edgedet {
 
 // ------------------------------------------------------------------------------ preprocess
 
-__global__ void preprocess_kernel(PreParams p) {
+// ObjectDetectionDataset.__getitem__'s `image / 255` (detect.py:55-58) on the device for a uint8
+// input: an IEEE float division (correctly rounded, as torch's CPU true_divide), so the value equals
+// the host's float image bit for bit and the rest of the transform is unchanged.
+template <typename T>
+__device__ __forceinline__ float pre_load(const T* src, int64_t i) {
+    if constexpr (sizeof(T) == 1) return (float)src[i] / 255.f;
+    else return src[i];
+}
+
+template <typename T>
+__global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
     if (idx >= total) return;
@@ -37,11 +47,11 @@ __global__ void preprocess_kernel(PreParams p) {
         float v[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float* src = p.x + ((int64_t)b * 3 + c) * p.H * p.W;
-            const float a00 = (src[(int64_t)y0 * p.W + x0] - p.mean[c]) / p.stdv[c];
-            const float a01 = (src[(int64_t)y0 * p.W + x1] - p.mean[c]) / p.stdv[c];
-            const float a10 = (src[(int64_t)y1 * p.W + x0] - p.mean[c]) / p.stdv[c];
-            const float a11 = (src[(int64_t)y1 * p.W + x1] - p.mean[c]) / p.stdv[c];
+            const T* src = x + ((int64_t)b * 3 + c) * p.H * p.W;
+            const float a00 = (pre_load(src, (int64_t)y0 * p.W + x0) - p.mean[c]) / p.stdv[c];
+            const float a01 = (pre_load(src, (int64_t)y0 * p.W + x1) - p.mean[c]) / p.stdv[c];
+            const float a10 = (pre_load(src, (int64_t)y1 * p.W + x0) - p.mean[c]) / p.stdv[c];
+            const float a11 = (pre_load(src, (int64_t)y1 * p.W + x1) - p.mean[c]) / p.stdv[c];
             v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
         }
         out = f32x4{v[0], v[1], v[2], 0.f};
@@ -51,12 +61,15 @@ __global__ void preprocess_kernel(PreParams p) {
 
 int preprocess_launch(const PreParams& p0, hipStream_t s) {
     PreParams p = p0;
-    EDGEDET_REQUIRE(p.x && p.y, "preprocess: null x/y");
+    EDGEDET_REQUIRE(p.y && ((p.x != nullptr) != (p.xu8 != nullptr)), "preprocess: null y, or not exactly one of x (f32) / x (u8)");
     EDGEDET_REQUIRE(p.Hp >= p.Ho && p.Wp >= p.Wo && p.Ho > 0 && p.Wo > 0, "preprocess: bad sizes");
     p.sh = (float)p.H / (float)p.Ho;
     p.sw = (float)p.W / (float)p.Wo;
     const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
-    hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p);
+    if (p.xu8)
+        hipLaunchKernelGGL(preprocess_kernel<uint8_t>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.xu8);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<float>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.x);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

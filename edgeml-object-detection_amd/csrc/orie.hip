@@ -255,40 +255,49 @@ struct BoxCorrectParams {
     uint8_t* tp;            // [n_det]
 };
 
+// Labels are processed in chunks of BC_CHUNK (the per-label LDS slots): every chunk recomputes each
+// detection's best label over ALL labels and keeps only the choices that fall in the chunk, so any
+// label count works (lib/metrics.py has no limit); one chunk (<= 1024 labels) is the common case.
+constexpr int BC_CHUNK = 1024;
+
 __global__ void __launch_bounds__(256) box_correct_kernel(BoxCorrectParams P) {
-    __shared__ int best_det[1024];  // per label: smallest detection index that chose it
+    __shared__ int best_det[BC_CHUNK];  // per label of the chunk: smallest detection index that chose it
     const int im = blockIdx.x;
     const int64_t d0 = P.det_off[im], d1 = P.det_off[im + 1];
     const int64_t l0 = P.lab_off[im], l1 = P.lab_off[im + 1];
     const int nd = (int)(d1 - d0), nl = (int)(l1 - l0);
     for (int d = threadIdx.x; d < nd; d += blockDim.x) P.tp[d0 + d] = 0;
     if (nl == 0 || nd == 0) return;
-    for (int l = threadIdx.x; l < nl; l += blockDim.x) best_det[l] = 0x7fffffff;
-    __syncthreads();
-    for (int d = threadIdx.x; d < nd; d += blockDim.x) {
-        const double* b2 = P.det + (d0 + d) * 4;
-        const int dc = P.det_cls[d0 + d];
-        const double a2 = (b2[2] - b2[0]) * (b2[3] - b2[1]);
-        double best = -1.0;
-        int bl = -1;
-        for (int l = 0; l < nl; ++l) {
-            if (P.lab_cls[l0 + l] != dc) continue;
-            const double* b1 = P.lab + (l0 + l) * 4;
-            const double x1 = fmax(b1[0], b2[0]), y1 = fmax(b1[1], b2[1]);
-            const double x2 = fmin(b1[2], b2[2]), y2 = fmin(b1[3], b2[3]);
-            const double inter = fmax(0.0, x2 - x1) * fmax(0.0, y2 - y1);
-            const double a1 = (b1[2] - b1[0]) * (b1[3] - b1[1]);
-            const double iou = inter / (a1 + a2 - inter);
-            if (iou >= P.thr && iou >= best) {  // ties -> the larger label index
-                best = iou;
-                bl = l;
+    for (int c0 = 0; c0 < nl; c0 += BC_CHUNK) {
+        const int cn = nl - c0 < BC_CHUNK ? nl - c0 : BC_CHUNK;
+        __syncthreads();  // the previous chunk's TP writes have read best_det
+        for (int l = threadIdx.x; l < cn; l += blockDim.x) best_det[l] = 0x7fffffff;
+        __syncthreads();
+        for (int d = threadIdx.x; d < nd; d += blockDim.x) {
+            const double* b2 = P.det + (d0 + d) * 4;
+            const int dc = P.det_cls[d0 + d];
+            const double a2 = (b2[2] - b2[0]) * (b2[3] - b2[1]);
+            double best = -1.0;
+            int bl = -1;
+            for (int l = 0; l < nl; ++l) {
+                if (P.lab_cls[l0 + l] != dc) continue;
+                const double* b1 = P.lab + (l0 + l) * 4;
+                const double x1 = fmax(b1[0], b2[0]), y1 = fmax(b1[1], b2[1]);
+                const double x2 = fmin(b1[2], b2[2]), y2 = fmin(b1[3], b2[3]);
+                const double inter = fmax(0.0, x2 - x1) * fmax(0.0, y2 - y1);
+                const double a1 = (b1[2] - b1[0]) * (b1[3] - b1[1]);
+                const double iou = inter / (a1 + a2 - inter);
+                if (iou >= P.thr && iou >= best) {  // ties -> the larger label index
+                    best = iou;
+                    bl = l;
+                }
             }
+            if (bl >= c0 && bl < c0 + cn) atomicMin(&best_det[bl - c0], d);
         }
-        if (bl >= 0) atomicMin(&best_det[bl], d);
+        __syncthreads();
+        for (int l = threadIdx.x; l < cn; l += blockDim.x)
+            if (best_det[l] != 0x7fffffff) P.tp[d0 + best_det[l]] = 1;
     }
-    __syncthreads();
-    for (int l = threadIdx.x; l < nl; l += blockDim.x)
-        if (best_det[l] != 0x7fffffff) P.tp[d0 + best_det[l]] = 1;
 }
 
 // lib/data.py:127-160 extract_output_feature for many images: the top-k rows (file order = score
@@ -319,9 +328,9 @@ using namespace edgedet;
 extern "C" int edgedet_box_correct(const double* det_xyxy, const int32_t* det_cls, const int64_t* det_off,
                                    const double* lab_xyxy, const int32_t* lab_cls, const int64_t* lab_off,
                                    int64_t n_img, double iou_thr, uint8_t* tp, int64_t max_labels, void* stream) {
+    (void)max_labels;  // any count: the kernel matches labels in 1024-label chunks
     EDGEDET_REQUIRE(det_off && lab_off && tp, "box_correct: null pointer");
     EDGEDET_REQUIRE(n_img >= 0 && n_img < (1ll << 31), "box_correct: bad image count");
-    EDGEDET_REQUIRE(max_labels <= 1024, "box_correct: more than 1024 labels in one image");
     if (n_img == 0) return 0;
     BoxCorrectParams P{det_xyxy, det_cls, det_off, lab_xyxy, lab_cls, lab_off, iou_thr, tp};
     hipLaunchKernelGGL(box_correct_kernel, dim3((unsigned)n_img), dim3(256), 0, (hipStream_t)stream, P);

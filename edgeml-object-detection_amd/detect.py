@@ -46,12 +46,19 @@ def load_weak_models(model_name: str, model_path: str, num_class: int):
     return models.RetinaNetFPNv2(sd, num_class)
 
 
-def read_image(path):
-    """torchvision.io.read_image(path, ImageReadMode.RGB) -> uint8 [3,H,W] (PIL decoder)."""
+def read_image(path, out=None):
+    """torchvision.io.read_image(path, ImageReadMode.RGB) -> uint8 [3,H,W] (PIL decoder); with `out`
+    the image is written into that [3,H,W] uint8 tensor (a slot of a pinned batch buffer)."""
     from PIL import Image
     with Image.open(path) as im:
         arr = np.asarray(im.convert("RGB"), dtype=np.uint8)
-    return torch.from_numpy(arr.copy()).permute(2, 0, 1).contiguous()
+    # the HWC -> CHW copy in numpy (single-threaded): this runs on the decode pool's threads, where a
+    # torch copy would start its own intra-op thread team per call (measured 10x slower on a
+    # 16-core share of a 256-core host)
+    if out is not None:
+        np.copyto(out.numpy(), arr.transpose(2, 0, 1))
+        return out
+    return torch.from_numpy(np.ascontiguousarray(arr.transpose(2, 0, 1)))
 
 
 class ObjectDetectionDataset:
@@ -65,8 +72,12 @@ class ObjectDetectionDataset:
         return len(self.img_names)
 
     def __getitem__(self, idx):
-        image = read_image(os.path.join(self.img_dir, self.img_names[idx]))
-        return image / 255
+        return self.read_u8(idx) / 255
+
+    def read_u8(self, idx, out=None):
+        """The decoded uint8 [3,H,W] image (detect.py:57) before its `/ 255` (detect.py:58): the CLI
+        uploads these bytes and the engine divides on the device, bit-identically."""
+        return read_image(os.path.join(self.img_dir, self.img_names[idx]), out)
 
 
 def _image_size(path):
@@ -76,11 +87,14 @@ def _image_size(path):
 
 
 def _decoded_batches(dataset, batch, workers=None):
-    """Yield (names, [3,H,W] float images) for batches of at most `batch` equal-size images: groups
-    by size in first-appearance order, names in sorted order within a group.  Decoding runs on a
-    thread pool with the next batch in flight while the caller uses the current one."""
+    """Yield (names, (H, W), uint8 [B,3,H,W] pinned batch) for batches of at most `batch` equal-size
+    images: groups by size in first-appearance order, names in sorted order within a group.  Each
+    image is decoded straight into its slot of the batch's pinned buffer (the engine uploads it as
+    is) on a thread pool (one thread per usable host core; PIL releases the GIL while decoding), with
+    the next two batches in flight while the caller uses the current one."""
     import concurrent.futures as cf
-    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    from .distributed import usable_cpus
+    workers = workers or usable_cpus()
     paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
     with cf.ThreadPoolExecutor(workers) as ex:
         sizes = list(ex.map(_image_size, paths))
@@ -88,13 +102,22 @@ def _decoded_batches(dataset, batch, workers=None):
         for i, hw in enumerate(sizes):
             groups.setdefault(hw, []).append(i)
         chunks = [idx[k:k + batch] for idx in groups.values() for k in range(0, len(idx), batch)]
-        fut = [ex.submit(lambda c=c: [dataset[i] for i in c]) for c in chunks[:2]]
+        pin = torch.cuda.is_available()
+
+        def sub(c):  # one future per image, so a batch decodes on many threads at once
+            h, w = sizes[c[0]]
+            buf = torch.empty((len(c), 3, h, w), dtype=torch.uint8, pin_memory=pin)
+            return buf, [ex.submit(dataset.read_u8, i, buf[k]) for k, i in enumerate(c)]
+
+        fut = [sub(c) for c in chunks[:2]]
         for j, c in enumerate(chunks):
-            imgs = fut[j].result()
+            buf, fs = fut[j]
+            for f in fs:
+                f.result()
             if j + 2 < len(chunks):
-                fut.append(ex.submit(lambda c=chunks[j + 2]: [dataset[i] for i in c]))
+                fut.append(sub(chunks[j + 2]))
             fut[j] = None
-            yield [dataset.img_names[i] for i in c], imgs
+            yield [dataset.img_names[i] for i in c], sizes[c[0]], buf
 
 
 def detect_rows(model, images, dataset="coco"):
@@ -130,12 +153,10 @@ def main(opts):
     # decoded by a thread pool one batch ahead of the engine (PIL releases the GIL while decoding).
     # Up to model.INFLIGHT batches on the device at once (run_batches), so one batch's NMS tail
     # overlaps the next batch's backbone.
-    sized = ((names, [(int(im.shape[-2]), int(im.shape[-1])) for im in imgs], imgs)
-             for names, imgs in _decoded_batches(dataset, batch))
-    tagged = (((names, hw), imgs) for names, hw, imgs in sized)
-    for (names, hw), dets in model.run_batches(tagged):
-        for name, (h, w), (b, s, l) in zip(names, hw, dets):
-            results[name] = fmt.format_detections(b, s, l, h, w, opts.dataset)
+    tagged = (((names, hw), buf) for names, hw, buf in _decoded_batches(dataset, batch))
+    for (names, (h, w)), counts, boxes, scores, labels in model.run_batches(tagged, raw=True):
+        for name, rows in zip(names, fmt.format_batch(boxes, scores, labels, counts, h, w, opts.dataset)):
+            results[name] = rows
     if world > 1:
         results = dist_mod.gather_rows(results, my_names, img_names, rank, world)
     if rank == 0:

@@ -41,6 +41,24 @@ def rank_world():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
+def usable_cpus():
+    """CPU cores this process may actually use: the affinity mask, further limited by a cgroup v2
+    CPU quota (cpu.max) when one is set.  os.cpu_count() reports the whole host, which on a shared
+    GPU box is many times the share a job gets, so thread pools are sized by this instead."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def local_rank():
     return int(os.environ.get("LOCAL_RANK", 0))
 

@@ -135,8 +135,11 @@ class _Detector:
         return ref
 
     # inference --------------------------------------------------------------------------------
-    def plan(self, B, H, W):
-        key = (int(B), int(H), int(W))
+    def plan(self, B, H, W, u8=False):
+        """The plan of (B, H, W).  u8: the input buffer holds the decoded uint8 images
+        (detect.py:57) and the transform divides by 255 on the device (bit-identical to the host's
+        `image / 255`, detect.py:58); otherwise it holds the model contract's float images."""
+        key = (int(B), int(H), int(W), bool(u8))
         if key not in self.plans:
             if self.device is None:
                 self.to("cuda")
@@ -177,62 +180,101 @@ class _Detector:
     INFLIGHT = 2  # batches on the device at once in run_batches (measured best on MI355X: bench --inflight)
 
     @torch.no_grad()
-    def run_batches(self, batches, inflight=None):
+    def run_batches(self, batches, inflight=None, raw=False):
         """Yield (tag, [(boxes, scores, labels) host numpy arrays per image]) for each (tag, images) of
-        `batches`, in order, with up to `inflight` batches on the device at once.  Each in-flight
-        slot owns an independent plan (arena + outputs) and a stream, so batch k+1's first layers run
-        under batch k's low-occupancy NMS tail; a slot is reused only after its results have been
-        copied to the host.  Same arithmetic as __call__ (same plan lowering, same kernels)."""
+        `batches`, in order, with up to `inflight` batches on the device at once (raw=True: yield
+        (tag, counts [B], boxes [B,K,4], scores [B,K], labels [B,K]) padded host arrays instead, the
+        input of fmt.format_batch).  `images` is a list of [3,H,W] tensors or one [B,3,H,W] tensor; a
+        pinned [B,3,H,W] tensor is uploaded as it is (no staging copy).  Each in-flight
+        slot owns an independent plan (arena + outputs), a stream and pinned host staging, so batch
+        k+1's upload and first layers run under batch k's low-occupancy NMS tail; a slot is reused
+        only after its results have been copied to the host.  Images are either the model
+        contract's float [3,H,W] tensors or the decoded uint8 [3,H,W] images (detect.py:57), which
+        cross PCIe as bytes (4x fewer than float) and are divided by 255 on the device, bit-identical
+        to the host's `image / 255` (detect.py:58).  Same arithmetic as __call__ (same plan
+        lowering, same kernels)."""
         if self.device is None:
             self.to("cuda")
         n = max(1, int(inflight or self.INFLIGHT))
-        slots = {}   # (B, H, W) -> [(plan, stream)] * n
-        pending = []  # (tag, plan, stream, B)
+        # (B, H, W, u8) -> [slot dict] * n, kept on the model across calls (the plans, streams and
+        # pinned buffers of a shape are built once)
+        slots = self.__dict__.setdefault("_slots", {})
+        for key in [k for k, v in slots.items() if len(v) != n]:
+            del slots[key]
+        pending = []  # (tag, slot, B)
         turn = [0]
 
-        def slot(B, H, W):
-            key = (B, H, W)
+        def new_slot(key, first):
+            B, H, W, u8 = key
+            plan = self.plan(*key) if first else self.build_plan(*key).finalize()
+            dt = torch.uint8 if u8 else torch.float32
+            return {"plan": plan, "stream": torch.cuda.Stream(self.device),
+                    "stage": torch.empty((B, 3, H, W), dtype=dt, pin_memory=True),
+                    "count": torch.empty((B,), dtype=torch.int32, pin_memory=True),
+                    "box": torch.empty(tuple(plan.out_box.shape), dtype=torch.float32, pin_memory=True),
+                    "score": torch.empty(tuple(plan.out_score.shape), dtype=torch.float32, pin_memory=True),
+                    "label": torch.empty(tuple(plan.out_label.shape), dtype=torch.int64, pin_memory=True),
+                    "done": torch.cuda.Event()}
+
+        def slot(key):
             if key not in slots:
-                first = self.plan(B, H, W)
-                slots[key] = [(first, torch.cuda.Stream(self.device))] + \
-                             [(self.build_plan(B, H, W).finalize(), torch.cuda.Stream(self.device))
-                              for _ in range(n - 1)]
+                slots[key] = [new_slot(key, k == 0) for k in range(n)]
             turn[0] += 1
             return slots[key][turn[0] % n]
 
-        def collect(tag, plan, stream, B):
-            stream.synchronize()
-            counts = plan.out_count.tensor().cpu().tolist()
-            box = plan.out_box.tensor().cpu().numpy()
-            score = plan.out_score.tensor().cpu().numpy()
-            label = plan.out_label.tensor().cpu().numpy()
+        def collect(tag, sl, B):
+            sl["done"].synchronize()
+            sl["src"] = None
+            if raw:
+                return tag, sl["count"].numpy().copy(), sl["box"].numpy().copy(), sl["score"].numpy().copy(), \
+                    sl["label"].numpy().copy()
+            counts = sl["count"].tolist()
+            box, score, label = sl["box"].numpy(), sl["score"].numpy(), sl["label"].numpy()
             return tag, [(box[j, :counts[j]].copy(), score[j, :counts[j]].copy(), label[j, :counts[j]].copy())
                          for j in range(B)]
 
         for tag, imgs in batches:
-            imgs = list(imgs)
-            shapes = {tuple(im.shape[-2:]) for im in imgs}
-            if len(shapes) != 1 or len(imgs) > self.max_batch:
-                raise ValueError("run_batches takes batches of <= max_batch equal-size images")
-            (H, W), B = shapes.pop(), len(imgs)
-            if slots and (B, H, W) not in slots:
+            whole = imgs if torch.is_tensor(imgs) and imgs.dim() == 4 else None
+            if whole is not None:
+                shapes, dtypes, B = {tuple(whole.shape[-2:])}, {whole.dtype}, whole.shape[0]
+            else:
+                imgs = list(imgs)
+                shapes, dtypes, B = {tuple(im.shape[-2:]) for im in imgs}, {im.dtype for im in imgs}, len(imgs)
+            if len(shapes) != 1 or len(dtypes) != 1 or B > self.max_batch or B == 0:
+                raise ValueError("run_batches takes batches of 1..max_batch equal-size images of one dtype")
+            H, W = shapes.pop()
+            key = (B, H, W, dtypes.pop() == torch.uint8)
+            if slots and key not in slots:
                 # a new shape: finish the old shape's batches and free its plans (the CLI groups
                 # images by size, so a real image set touches each shape in one run of batches)
                 while pending:
                     yield collect(*pending.pop(0))
-                for key in slots:
-                    self.plans.pop(key, None)
+                for k in slots:
+                    self.plans.pop(k, None)
                 slots.clear()
-            plan, stream = slot(B, H, W)
+            sl = slot(key)
             # the slot's previous batch (if any) must be on the host before its buffers are reused
-            while any(p is plan for _, p, _, _ in pending):
+            while any(p is sl for _, p, _ in pending):
                 yield collect(*pending.pop(0))
+            plan, stream = sl["plan"], sl["stream"]
+            stage = sl["stage"]
+            sl["done"].synchronize()  # a slot left in flight by an abandoned earlier call
+            if whole is not None and whole.is_pinned() and whole.dtype in (torch.uint8, torch.float32) \
+                    and whole.is_contiguous():
+                src = sl["src"] = whole  # held until the slot is collected (the copy is asynchronous)
+            else:
+                for j, im in enumerate(whole if whole is not None else imgs):
+                    stage[j].copy_(im if key[3] else im.to(torch.float32))
+                src = stage
             with torch.cuda.stream(stream):
-                inp = plan.input.tensor()
-                for j, im in enumerate(imgs):
-                    inp[j].copy_(im.to(self.device, torch.float32), non_blocking=True)
+                plan.input.tensor().copy_(src, non_blocking=True)
                 plan.run(stream)
-            pending.append((tag, plan, stream, B))
+                sl["count"].copy_(plan.out_count.tensor(), non_blocking=True)
+                sl["box"].copy_(plan.out_box.tensor(), non_blocking=True)
+                sl["score"].copy_(plan.out_score.tensor(), non_blocking=True)
+                sl["label"].copy_(plan.out_label.tensor(), non_blocking=True)
+                sl["done"].record(stream)
+            pending.append((tag, sl, B))
             while len(pending) >= n:
                 yield collect(*pending.pop(0))
         while pending:
@@ -293,10 +335,10 @@ class SSDLite320(_Detector):
         starts = [c * q + min(c, r) for c in range(n)]
         return [(b0, q + (1 if c < r else 0)) for c, b0 in enumerate(starts)]
 
-    def build_plan(self, B, H, W, pack_only=False):
+    def build_plan(self, B, H, W, u8=False, pack_only=False):
         P = Plan(self.pack, self.device or "cpu")
         nch = 1 if pack_only else self.n_chains(B)
-        inp = P.buf((B, 3, H, W), name="images")
+        inp = P.buf((B, 3, H, W), torch.uint8 if u8 else torch.float32, name="images")
         shared = {}
         if nch > 1:
             P.fork(nch - 1)
@@ -323,7 +365,8 @@ class SSDLite320(_Detector):
         sfx = f"#{c}" if nch > 1 else ""
         view = (lambda buf: BufView(buf, img0, B)) if nch > 1 else (lambda buf: buf)
         x = P.buf((B, S, S, 4), name="pre" + sfx)
-        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {0: view(inp), 1: x},
+        src = {2: view(inp)} if inp.dtype == torch.uint8 else {0: view(inp)}
+        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: S, 4: S, 5: S, 6: S}, {**src, 1: x},
                  {0: 0.5, 1: 0.5, 2: 0.5, 3: 0.5, 4: 0.5, 5: 0.5}, name="transform"))
         cur = (x, (B, S, S, 4))
 
@@ -550,15 +593,15 @@ class FasterRCNNFPNv2(_Detector):
         scale = min(float(self.MIN_SIZE) / min(H, W), float(self.MAX_SIZE) / max(H, W))
         return int(math.floor(H * scale)), int(math.floor(W * scale))
 
-    def _lower_body(self, P, B, H, W):
+    def _lower_body(self, P, B, H, W, u8=False):
         """GeneralizedRCNNTransform + ResNet-50 body (shared with RetinaNet): returns the input buffer,
         the sizes, the conv / maxpool emitters and C2..C5."""
         Ho, Wo = self.resized_size(H, W)
         Hp = (Ho + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
         Wp = (Wo + self.DIVISIBLE - 1) // self.DIVISIBLE * self.DIVISIBLE
-        inp = P.buf((B, 3, H, W), name="images")
+        inp = P.buf((B, 3, H, W), torch.uint8 if u8 else torch.float32, name="images")
         x = P.buf((B, Hp, Wp, 4), name="pre")
-        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: Ho, 4: Wo, 5: Hp, 6: Wp}, {0: inp, 1: x},
+        P.add(Op(ops.PREPROCESS, {0: B, 1: H, 2: W, 3: Ho, 4: Wo, 5: Hp, 6: Wp}, {(2 if u8 else 0): inp, 1: x},
                  {0: self.MEAN[0], 1: self.MEAN[1], 2: self.MEAN[2], 3: self.STD[0], 4: self.STD[1],
                   5: self.STD[2]}, name="transform"))
         cur = (x, (B, Hp, Wp, 4))
@@ -622,10 +665,10 @@ class FasterRCNNFPNv2(_Detector):
 
         return inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs
 
-    def build_plan(self, B, H, W, pack_only=False):
+    def build_plan(self, B, H, W, u8=False, pack_only=False):
         P = Plan(self.pack, self.device or "cpu")
         NC = self.num_classes
-        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W)
+        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W, u8)
 
         # ---- FPN (BN, no activations) + LastLevelMaxPool
         f = "backbone.fpn."
@@ -777,10 +820,10 @@ class RetinaNetFPNv2(FasterRCNNFPNv2):
             self._w[key] = (self.pack.add(_np(self.sd[p + ".weight"])), self.pack.add(_np(self.sd[p + ".bias"])))
         return self._w[key]
 
-    def build_plan(self, B, H, W, pack_only=False):
+    def build_plan(self, B, H, W, u8=False, pack_only=False):
         P = Plan(self.pack, self.device or "cpu")
         K, A = self.num_classes, self.A
-        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W)
+        inp, (Ho, Wo, Hp, Wp), conv, maxpool, cs = self._lower_body(P, B, H, W, u8)
         f = "backbone.fpn."
         c3, c4, c5 = cs[1], cs[2], cs[3]
         last = conv(c5, f + "inner_blocks.2.0.weight", None, 1, 1, None, bias_key=f + "inner_blocks.2.0.bias")

@@ -76,8 +76,6 @@ def box_correct_batch(dets, labels, iou_thr=0.5, device="cuda"):
     dcls = np.concatenate([d[0] for d in dets if len(d)] or [np.zeros(0)]).astype(np.int32)
     lbox = np.concatenate([l[1] for l in labels if len(l)] or [np.zeros((0, 4))]).astype(np.float64)
     lcls = np.concatenate([l[0] for l in labels if len(l)] or [np.zeros(0)]).astype(np.int32)
-    if int(ln.max(initial=0)) > 1024:
-        raise ValueError("box_correct: an image has more than 1024 ground-truth boxes")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
     g_dbox, g_dcls, g_doff, g_lbox, g_lcls, g_loff = (t(a) for a in (dbox if len(dbox) else np.zeros((1, 4)),
                                                                       dcls if len(dcls) else np.zeros(1, np.int32),

@@ -166,9 +166,14 @@ def make_scene(seed, h=640, w=640, return_boxes=False):
     return (img, boxes) if return_boxes else img
 
 
+def make_batch_u8(n, h=640, w=640, seed=0):
+    """uint8 [n,3,h,w]: the decoded images (detect.py:57) of make_batch."""
+    return torch.from_numpy(np.stack([make_scene(seed + i, h, w) for i in range(n)]))
+
+
 def make_batch(n, h=640, w=640, seed=0):
     """float32 [n,3,h,w] in [0,1] (the detect.py:58 input contract)."""
-    return torch.from_numpy(np.stack([make_scene(seed + i, h, w) for i in range(n)])).float() / 255
+    return make_batch_u8(n, h, w, seed).float() / 255
 
 
 def make_dataset(img_dir, n, seed=0, label_dir=None, sizes=COCO_SIZES, ext=".png"):

@@ -201,7 +201,8 @@ int edgedet_conv_tile(const edgedet_op* op);
  * lib/metrics.py box_correct (lib/data.py set_data's TP flags) for many images at once: detections
  * det_xyxy [n_det][4] f64 + det_cls, labels lab_xyxy [n_lab][4] f64 + lab_cls, both grouped per image
  * by the offsets det_off / lab_off [n_img + 1]; tp [n_det] = 1 where the detection is matched at
- * IoU >= iou_thr.  max_labels = the most labels of any one image (<= 1024).
+ * IoU >= iou_thr.  max_labels = the most labels of any one image (any count; images with more than
+ * 1024 labels are matched in 1024-label chunks).
  */
 int edgedet_box_correct(const double* det_xyxy, const int32_t* det_cls, const int64_t* det_off,
                         const double* lab_xyxy, const int32_t* lab_cls, const int64_t* lab_off,

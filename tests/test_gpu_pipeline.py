@@ -130,28 +130,35 @@ def test_detect_then_reward_cli_equals_oracle_pipeline():
 
 @pytest.mark.parametrize("kind", ["ssd", "frcnn"])
 def test_run_batches_matches_call(kind):
-    """model.run_batches (the CLI's path: two batches in flight, each on its own plan instance and
-    stream) gives bit-identical detections to model(images) batch by batch, across a shape change,
-    a ragged last batch and slot reuse."""
+    """model.run_batches (the CLI's path: two batches in flight, each on its own plan instance,
+    stream and side lanes) gives bit-identical detections to model(images) batch by batch, across a
+    shape change, a ragged last batch and slot reuse; the decoded uint8 images (divided by 255 on
+    the device) give the same detections as the host's float images.  The SSD case includes 16-image
+    batches (two chains on side lanes) with both in-flight instances busy at once."""
     from edgeml_amd import models, synthetic
     if kind == "ssd":
         sd = synthetic.synthetic_state_dict("ssd", 91, True, seed=0)
         model = models.SSDLite320(sd, 91, True).to("cuda:0")
+        shapes = [(480, 640, 2)] * 2 + [(480, 640, 1)] + [(640, 640, 16)] * 3
     else:
         model = models.fasterrcnn_resnet50_fpn_v2().to("cuda:0")
-    shapes = [(480, 640)] * 3 + [(640, 640)] * 2
-    batches = []
-    for i, (h, w) in enumerate(shapes):
-        n = 1 if i == 2 else 2
-        imgs = synthetic.make_batch(n, h, w, seed=40 + i)
-        batches.append((i, list(imgs)))
+        shapes = [(480, 640, 2)] * 2 + [(480, 640, 1)] + [(640, 640, 2)] * 2
+    batches, batches_u8 = [], []
+    for i, (h, w, n) in enumerate(shapes):
+        u8 = synthetic.make_batch_u8(n, h, w, seed=40 + i)
+        batches.append((i, list(u8.float() / 255)))
+        batches_u8.append((i, list(u8)))
     got = list(model.run_batches(batches, inflight=2))
-    assert [t for t, _ in got] == list(range(len(batches)))
-    for (tag, dets), (_, imgs) in zip(got, batches):
+    got_u8 = list(model.run_batches(batches_u8, inflight=2))
+    assert [t for t, _ in got] == list(range(len(batches))) == [t for t, _ in got_u8]
+    for (tag, dets), (_, dets_u8), (_, imgs) in zip(got, got_u8, batches):
         ref = model(imgs)
-        assert len(dets) == len(imgs)
-        for (b, s, l), r in zip(dets, ref):
+        assert len(dets) == len(imgs) == len(dets_u8)
+        for (b, s, l), (bu, su, lu), r in zip(dets, dets_u8, ref):
             np.testing.assert_array_equal(b, r["boxes"].cpu().numpy())
             np.testing.assert_array_equal(s, r["scores"].cpu().numpy())
             np.testing.assert_array_equal(l, r["labels"].cpu().numpy())
+            np.testing.assert_array_equal(bu, b)
+            np.testing.assert_array_equal(su, s)
+            np.testing.assert_array_equal(lu, l)
             assert len(s) > 0

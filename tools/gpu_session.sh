@@ -21,12 +21,12 @@ step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench 600 python -u bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = "1" ]; then
-step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o trace -- python3 bench.py --model all --no-cpu
+step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o trace -- python3 bench.py --model all --no-cpu --no-e2e
 fi
 if [ "${PMC:-1}" = "1" ]; then
 for m in ssd frcnn; do
-  step bench_fetch_$m 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$m -o fetch -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu
-  step bench_write_$m 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$m -o write -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu
+  step bench_fetch_$m 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$m -o fetch -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu --no-e2e
+  step bench_write_$m 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$m -o write -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu --no-e2e
   python tools/pmc_summary.py --bench-log gpurun_out/bench_fetch_$m.log --model $m --fetch gpurun_out/prof_fetch_$m --write gpurun_out/prof_write_$m -o gpurun_out/pmc_$m.json >> gpurun_out/steps.log 2>&1
 done
 fi
