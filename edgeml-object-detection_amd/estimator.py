@@ -89,6 +89,15 @@ class MlpSpec:
                 s[e["rv"]:e["rv"] + dout] = 1.0
         return s
 
+    def pack(self, named):
+        """The inverse of unpack: a state vector from EdgeDetectionNet-named arrays (a reference
+        state_dict, num_batches_tracked ignored)."""
+        s = np.zeros(self.ns, np.float32)
+        ref = self.unpack(s)
+        for k, v in ref.items():
+            v[...] = np.asarray(named[k], np.float32).reshape(v.shape)  # views into s
+        return s
+
     def unpack(self, state):
         """{name: array} in torch's EdgeDetectionNet naming (linear_stacks.<l>.<0|1>.*)."""
         out = {}

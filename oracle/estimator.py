@@ -9,8 +9,10 @@ Restatement, on PyTorch-CPU, of the stage-24 ORIE estimator training (SURVEY.md 
                    :335-342, estimates of the best and the last model :307-323
 The weights start from a given state vector (edgeml_amd.estimator.MlpSpec layout) instead of
 torch's RNG, and dropout can be switched off, so a GPU fit can be compared step for step.
-Parity pinning: the reference module's behaviour is torch's own nn / optim code, which this file
-calls directly (no reference-generated fixtures exist for training: "parity unpinned" beyond that).
+Parity pinning: tests/golden/g4_estimator.npz holds the reference's own fit_CNN run on its own
+EdgeDetectionNet (tests/golden/make_golden_estimator.py; dropout off, the reference's initial
+weights): from those weights this restatement reproduces the reference's best / last estimates and
+best state bit for bit (tests/test_golden.py::test_estimator_oracle_matches_reference_fit).
 """
 import copy
 

@@ -117,3 +117,29 @@ def test_cli_writes_regression_estimate_files():
                     assert set(z.files) == {"train_est", "val_est", "train_time", "val_time"}
                     assert z["train_est"].shape == ((~split[k]).sum(),)
                     assert z["val_est"].shape == (split[k].sum(),)
+
+
+@pytest.mark.parametrize("case", ["mse", "weighted"])
+def test_fit_from_reference_weights_matches_reference(case):
+    """The device fit from the reference's own initial weights (G4: regression.py fit_CNN on
+    lib/nn_model.py's EdgeDetectionNet, dropout off) ends at the reference's estimates: the best
+    and last models' train / val estimates within fp32-training tolerance of the reference's."""
+    from edgeml_amd import estimator
+    here = os.path.dirname(os.path.abspath(__file__))
+    with np.load(os.path.join(here, "golden", "g4_estimator.npz"), allow_pickle=False) as z:
+        g = {k[len(case) + 1:]: z[k] for k in z.files if k.startswith(case + "/")}
+    ntr, nva, weight, epochs, batch = (int(v) for v in g["cfg"])
+    dims = [int(v) for v in g["linear"]]
+    spec = estimator.MlpSpec(dims)
+    init = spec.pack({k[5:]: v for k, v in g.items() if k.startswith("init/")})
+    opts = estimator.CNNOpt(max_epoch=epochs, batch_size=batch, weight=bool(weight),
+                            milestones=[int(m) for m in g["milestones"]], hidden=dims[1:-1], dropout=0.0)
+    split = np.zeros((1, ntr + nva), bool)
+    split[0, ntr:] = True
+    best, last, _ = estimator.fit_folds(g["x"], g["y"], split, opts, init=init[None])
+    tol = 0.02 * float(np.std(g["y"]))
+    for tag, got in (("best", best[0]), ("last", last[0])):
+        for k in ("train_est", "val_est"):
+            d = float(np.abs(got[k] - g[f"{tag}/{k}"]).max())
+            print(case, tag, k, "max |d| vs reference", d)
+            assert d <= tol, (case, tag, k, d, tol)
