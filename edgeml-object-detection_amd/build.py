@@ -30,9 +30,25 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
+TILES_JSON = os.path.join(HERE, "data", "conv_tiles_gfx950.json")
+
+
 def _deps():
     return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")] + [
-        os.path.join(os.path.dirname(HERE), "include", "edgedet.h")]
+        os.path.join(os.path.dirname(HERE), "include", "edgedet.h"), TILES_JSON]
+
+
+def write_tile_table(objdir):
+    """The tuned conv tile table (data/conv_tiles_gfx950.json, also read by plan.py) as a C++
+    initializer list for the native lowering (csrc/lower.hip)."""
+    import json
+    with open(TILES_JSON) as f:
+        tiles = json.load(f).get("tiles", {})
+    path = os.path.join(objdir, "conv_tiles_gfx950.inc")
+    body = "".join(f'{{"{k}", {int(v)}}},\n' for k, v in sorted(tiles.items()))
+    if not os.path.exists(path) or open(path).read() != body:
+        with open(path, "w") as f:
+            f.write(body)
 
 
 def up_to_date():
@@ -48,10 +64,11 @@ def build(force=False, verbose=False, jobs=8):
     cc = hipcc()
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
+    write_tile_table(objdir)
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
-        cmd = [cc, *FLAGS, "-c", src, "-o", obj]
+        cmd = [cc, *FLAGS, "-I", objdir, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -45,7 +45,11 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
            "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds", "edgedet_ssd_stem",
-           "edgedet_mlp_state_size", "edgedet_mlp_fit", "edgedet_mlp_predict")
+           "edgedet_mlp_state_size", "edgedet_mlp_fit", "edgedet_mlp_predict",
+           "edgedet_model_weights_size", "edgedet_model_pack", "edgedet_model_workspace_size", "edgedet_model_prepare",
+           "edgedet_model_prepare_host", "edgedet_model_forward", "edgedet_model_max_detections",
+           "edgedet_model_records", "edgedet_ssdlite_workspace_size", "edgedet_ssdlite_forward",
+           "edgedet_frcnn_workspace_size", "edgedet_frcnn_forward")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -94,6 +98,26 @@ def lib():
                                   _vp, _i32, _i32, ctypes.c_float, ctypes.c_float, _vp, _i32, ctypes.c_float, _i32,
                                   ctypes.c_float, ctypes.c_uint64, _vp]
     L.edgedet_mlp_predict.argtypes = [_vp, _i64, _vp, _i64, _i32, _vp, _vp, _vp, _vp]
+    _u64 = ctypes.c_uint64
+    L.edgedet_model_weights_size.argtypes = [_i32, _i32, _i32]
+    L.edgedet_model_weights_size.restype = _i64
+    L.edgedet_model_pack.argtypes = [_i32, _i32, _i32, _i64, _vp, _vp, _vp, _vp]
+    L.edgedet_model_workspace_size.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32]
+    L.edgedet_model_workspace_size.restype = _i64
+    L.edgedet_model_prepare.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]
+    L.edgedet_model_prepare_host.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64]
+    L.edgedet_model_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                                        _vp]
+    L.edgedet_model_max_detections.argtypes = [_i32]
+    L.edgedet_model_records.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _u64, _u64, _u64, _u64, _u64, _u64,
+                                        _u64, _vp, _i64]
+    L.edgedet_model_records.restype = _i64
+    L.edgedet_ssdlite_workspace_size.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32]
+    L.edgedet_ssdlite_workspace_size.restype = _i64
+    L.edgedet_ssdlite_forward.argtypes = [_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.edgedet_frcnn_workspace_size.argtypes = [_i32, _i32, _i32, _i32, _i32]
+    L.edgedet_frcnn_workspace_size.restype = _i64
+    L.edgedet_frcnn_forward.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.edgedet_ssd_stem.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]
     L.edgedet_mbconv_front_lds.restype = ctypes.c_int64
     L.edgedet_mbconv_front.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32, _i32,

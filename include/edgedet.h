@@ -84,6 +84,62 @@ int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** 
 int edgedet_graph_launch(void* graph, void* stream);
 int edgedet_graph_destroy(void* graph);
 
+/* ------------------------------------------------------------------------ model forward */
+/*
+ * The detector call of torch_models/detect.py:78 (model(images) -> boxes / scores / labels for the
+ * models load_weak_models builds, detect.py:15-42), natively: the library lowers the detector into
+ * the same static plan the Python host builds (edgeml_amd/models.py; results bit-identical to it).
+ *   kind         EDGEDET_MODEL_SSDLITE (ssdlite320_mobilenet_v3_large, detect.py:24/26; reduced_tail
+ *                1 = the COCO-pretrained variant, 0 = the --model-path / train.py variant) or
+ *                EDGEDET_MODEL_FRCNN (fasterrcnn_resnet50_fpn_v2, detect.py:30/32; reduced_tail unused)
+ *   num_classes  91 (coco) or 21 (voc), detect.py:67
+ * Weights: edgedet_model_pack packs torchvision-named host tensors (a state_dict: names, fp32 values,
+ * element counts; num_batches_tracked may be omitted) into a blob of edgedet_model_weights_size bytes
+ * (BatchNorm folded, conv weights repacked and split into bf16 planes), which the caller copies to
+ * the device once.  Images: B x [3, H, W], float in [0, 1] (input_u8 = 0, detect.py:58) or the
+ * decoded uint8 bytes (input_u8 = 1, divided by 255 on the device, bit-identical).  Workspace:
+ * caller-owned device memory of edgedet_model_workspace_size bytes for (B, H, W, input_u8), set up
+ * once by edgedet_model_prepare (writes the anchors / rescale constants; synchronous).  Outputs:
+ * count [B] int32, boxes [B][K][4] xyxy float in original pixels, scores [B][K] descending,
+ * labels [B][K] int64, K = edgedet_model_max_detections(kind) (300 SSD / 100 FRCNN), the first
+ * count[b] rows valid (detect.py:79-81).  forward is asynchronous on `stream`.
+ */
+enum { EDGEDET_MODEL_SSDLITE = 0, EDGEDET_MODEL_FRCNN = 1 };
+int64_t edgedet_model_weights_size(int32_t kind, int32_t num_classes, int32_t reduced_tail);
+int edgedet_model_pack(int32_t kind, int32_t num_classes, int32_t reduced_tail, int64_t n_params,
+                       const char* const* names, const float* const* host_values, const int64_t* numels,
+                       void* host_blob);
+int64_t edgedet_model_workspace_size(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B,
+                                     int32_t H, int32_t W, int32_t input_u8);
+int edgedet_model_prepare(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                          int32_t W, int32_t input_u8, void* workspace, void* stream);
+/* edgedet_model_prepare into a host image of the workspace (bytes >= the workspace size): the
+ * constants at their offsets, nothing else written (host-side checks and staging). */
+int edgedet_model_prepare_host(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                               int32_t W, int32_t input_u8, void* host_workspace, int64_t bytes);
+int edgedet_model_forward(int32_t kind, int32_t num_classes, int32_t reduced_tail, const void* weights,
+                          const void* images, int32_t B, int32_t H, int32_t W, int32_t input_u8,
+                          void* workspace, int32_t* count, float* boxes, float* scores, int64_t* labels,
+                          void* stream);
+int edgedet_model_max_detections(int32_t kind);
+/* The op records forward would run (for graph capture: edgedet_graph_create on them, and for tests);
+ * pointers resolved against the given bases (0 = the workspace's own region for images / outputs).
+ * Returns the record count; fills out[] when cap is large enough. */
+int64_t edgedet_model_records(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                              int32_t W, int32_t input_u8, uint64_t weights, uint64_t workspace,
+                              uint64_t images, uint64_t count, uint64_t boxes, uint64_t scores,
+                              uint64_t labels, edgedet_op* out, int64_t cap);
+/* The per-detector names: the calls above with kind fixed. */
+int64_t edgedet_ssdlite_workspace_size(int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                                       int32_t W, int32_t input_u8);
+int edgedet_ssdlite_forward(const void* weights, int32_t num_classes, int32_t reduced_tail, const void* images,
+                            int32_t B, int32_t H, int32_t W, int32_t input_u8, void* workspace,
+                            int32_t* count, float* boxes, float* scores, int64_t* labels, void* stream);
+int64_t edgedet_frcnn_workspace_size(int32_t num_classes, int32_t B, int32_t H, int32_t W, int32_t input_u8);
+int edgedet_frcnn_forward(const void* weights, int32_t num_classes, const void* images, int32_t B, int32_t H,
+                          int32_t W, int32_t input_u8, void* workspace, int32_t* count, float* boxes,
+                          float* scores, int64_t* labels, void* stream);
+
 /* ------------------------------------------------------------------------ unit operators */
 /*
  * torchvision::nms (reference call sites: SSD postprocess, RPN filter_proposals and RoIHeads

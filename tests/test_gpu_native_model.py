@@ -1,0 +1,91 @@
+"""The model-level C-ABI on the GPU: edgedet_model_forward / edgedet_ssdlite_forward /
+edgedet_frcnn_forward (weights packed by edgedet_model_pack, caller-owned workspace and outputs)
+give detections bit-identical to the Python model object (detect.py:78's contract), for float and
+uint8 inputs, and a hipGraph captured from edgedet_model_records replays to the same results."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from edgeml_amd import models, native, ops, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(got, ref):
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        for k in ("boxes", "scores", "labels"):
+            np.testing.assert_array_equal(g[k].cpu().numpy(), r[k].cpu().numpy(), err_msg=k)
+        assert len(r["scores"]) > 0
+
+
+@pytest.mark.parametrize("kind,B,H,W", [("ssd", 2, 480, 640), ("ssd", 16, 640, 640), ("faster_rcnn", 2, 612, 612)])
+def test_native_forward_bit_identical_to_model(kind, B, H, W):
+    sd = synthetic.synthetic_state_dict(kind, 91, True, seed=0)
+    m = (models.SSDLite320(sd, 91, True) if kind == "ssd" else models.FasterRCNNFPNv2(sd, 91)).to("cuda")
+    nat = native.NativeDetector(kind, native.pack_state_dict(kind, sd, 91, True), 91, True).to("cuda")
+    u8 = synthetic.make_batch_u8(B, H, W, seed=11)
+    ref = m(list(u8.float() / 255))
+    _same(nat(u8.float() / 255), ref)
+    _same(nat(u8), ref)  # uint8 bytes, /255 on the device
+
+
+def test_per_model_entries_and_graph_replay():
+    """edgedet_ssdlite_forward with raw pointers, then the same records captured into a hipGraph."""
+    sd = synthetic.synthetic_state_dict("ssd", 91, True, seed=0)
+    m = models.SSDLite320(sd, 91, True).to("cuda")
+    B, H, W = 4, 427, 640
+    x = synthetic.make_batch(B, H, W, seed=21).cuda()
+    ref = m(list(x))
+    L = ops.lib()
+    wts = torch.from_numpy(native.pack_state_dict("ssd", sd, 91, True)).cuda()
+    ws = torch.zeros(L.edgedet_ssdlite_workspace_size(91, 1, B, H, W, 0), dtype=torch.uint8, device="cuda")
+    ops.check(L.edgedet_model_prepare(0, 91, 1, B, H, W, 0, ws.data_ptr(), ops.stream_handle()))
+    K = L.edgedet_model_max_detections(0)
+    outs = [torch.zeros(B, dtype=torch.int32, device="cuda"), torch.zeros((B, K, 4), device="cuda"),
+            torch.zeros((B, K), device="cuda"), torch.zeros((B, K), dtype=torch.int64, device="cuda")]
+    ops.check(L.edgedet_ssdlite_forward(wts.data_ptr(), 91, 1, x.data_ptr(), B, H, W, 0, ws.data_ptr(),
+                                        *[o.data_ptr() for o in outs], ops.stream_handle()))
+
+    def dets():
+        n = outs[0].cpu().tolist()
+        return [{"boxes": outs[1][b, :n[b]], "scores": outs[2][b, :n[b]], "labels": outs[3][b, :n[b]]}
+                for b in range(B)]
+    _same(dets(), ref)
+    for o in outs:
+        o.zero_()
+    rec = native.records("ssd", B, H, W, wts.data_ptr(), ws.data_ptr(), 91, True, False, x.data_ptr(),
+                         tuple(o.data_ptr() for o in outs))
+    s = torch.cuda.Stream()
+    g = ctypes.c_void_p()
+    ops.check(L.edgedet_graph_create(rec.ctypes.data_as(ctypes.c_void_p), len(rec), ops.stream_handle(s),
+                                     ctypes.byref(g)))
+    try:
+        ops.check(L.edgedet_graph_launch(g, ops.stream_handle(s)))
+        s.synchronize()
+        _same(dets(), ref)
+    finally:
+        L.edgedet_graph_destroy(g)
+
+
+def test_frcnn_entry_matches_model():
+    sd = synthetic.synthetic_state_dict("faster_rcnn", 91, seed=0)
+    m = models.FasterRCNNFPNv2(sd, 91).to("cuda")
+    B, H, W = 1, 480, 640
+    u8 = synthetic.make_batch_u8(B, H, W, seed=31)
+    ref = m(list(u8.float() / 255))
+    L = ops.lib()
+    wts = torch.from_numpy(native.pack_state_dict("faster_rcnn", sd, 91)).cuda()
+    ws = torch.zeros(L.edgedet_frcnn_workspace_size(91, B, H, W, 1), dtype=torch.uint8, device="cuda")
+    ops.check(L.edgedet_model_prepare(1, 91, 1, B, H, W, 1, ws.data_ptr(), ops.stream_handle()))
+    K = L.edgedet_model_max_detections(1)
+    x = u8.cuda()
+    outs = [torch.zeros(B, dtype=torch.int32, device="cuda"), torch.zeros((B, K, 4), device="cuda"),
+            torch.zeros((B, K), device="cuda"), torch.zeros((B, K), dtype=torch.int64, device="cuda")]
+    ops.check(L.edgedet_frcnn_forward(wts.data_ptr(), 91, x.data_ptr(), B, H, W, 1, ws.data_ptr(),
+                                      *[o.data_ptr() for o in outs], ops.stream_handle()))
+    n = outs[0].cpu().tolist()
+    _same([{"boxes": outs[1][b, :n[b]], "scores": outs[2][b, :n[b]], "labels": outs[3][b, :n[b]]}
+           for b in range(B)], ref)
