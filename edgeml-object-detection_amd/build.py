@@ -52,7 +52,7 @@ def write_tile_table(objdir):
 
 
 def up_to_date():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(os.path.join(os.path.dirname(HERE), "tools", "native_host")):
         return False
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(d) <= t for d in _deps())
@@ -83,7 +83,26 @@ def build(force=False, verbose=False, jobs=8):
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, LIB)
+    build_native_host(cc)
     return LIB
+
+
+HOST_SRC = os.path.join(os.path.dirname(HERE), "tools", "native_host.cpp")
+HOST_BIN = os.path.join(os.path.dirname(HERE), "tools", "native_host")
+
+
+def build_native_host(cc=None):
+    """tools/native_host: a C++ program (no Python) that runs a detector through the model-level
+    C-ABI, linked against the in-tree libedgedet.so (rpath relative to the binary)."""
+    if not os.path.exists(HOST_SRC):
+        return None
+    cc = cc or hipcc()
+    cmd = [cc, "-O2", "-std=c++17", HOST_SRC, "-I", os.path.join(os.path.dirname(HERE), "include"), "-L", HERE,
+           "-ledgedet", "-Wl,-rpath,$ORIGIN/../edgeml-object-detection_amd", "-o", HOST_BIN]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native_host build failed:\n{r.stderr}")
+    return HOST_BIN
 
 
 if __name__ == "__main__":

@@ -89,3 +89,32 @@ def test_frcnn_entry_matches_model():
     n = outs[0].cpu().tolist()
     _same([{"boxes": outs[1][b, :n[b]], "scores": outs[2][b, :n[b]], "labels": outs[3][b, :n[b]]}
            for b in range(B)], ref)
+
+
+@pytest.mark.parametrize("kind,B,H,W,u8", [("ssd", 3, 480, 640, 1), ("faster_rcnn", 1, 640, 480, 0)])
+def test_non_python_host_matches_model(kind, B, H, W, u8, tmp_path):
+    """tools/native_host (C++ against include/edgedet.h, no Python in the process) reads the packed
+    weights and the raw images, runs edgedet_model_forward and writes raw outputs: bit-identical to
+    the Python model object's detections."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "native_host")
+    assert os.path.exists(exe), "tools/native_host is built by __graft_entry__.build()"
+    sd = synthetic.synthetic_state_dict(kind, 91, True, seed=0)
+    m = (models.SSDLite320(sd, 91, True) if kind == "ssd" else models.FasterRCNNFPNv2(sd, 91)).to("cuda")
+    imgs = synthetic.make_batch_u8(B, H, W, seed=41)
+    ref = m(list(imgs.float() / 255))
+    (tmp_path / "w.bin").write_bytes(native.pack_state_dict(kind, sd, 91, True).tobytes())
+    (tmp_path / "x.bin").write_bytes((imgs if u8 else imgs.float() / 255).numpy().tobytes())
+    r = subprocess.run([exe, str(native._kind(kind)), "91", "1", str(B), str(H), str(W), str(u8),
+                        str(tmp_path / "w.bin"), str(tmp_path / "x.bin"), str(tmp_path / "out")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    print(r.stdout.strip())
+    K = ops.lib().edgedet_model_max_detections(native._kind(kind))
+    cnt = np.fromfile(tmp_path / "out.count", np.int32)
+    box = np.fromfile(tmp_path / "out.boxes", np.float32).reshape(B, K, 4)
+    sc = np.fromfile(tmp_path / "out.scores", np.float32).reshape(B, K)
+    lb = np.fromfile(tmp_path / "out.labels", np.int64).reshape(B, K)
+    _same([{"boxes": torch.from_numpy(box[b, :cnt[b]]), "scores": torch.from_numpy(sc[b, :cnt[b]]),
+            "labels": torch.from_numpy(lb[b, :cnt[b]])} for b in range(B)], ref)
