@@ -1447,6 +1447,8 @@ extern "C" int edgedet_model_prepare(int32_t kind, int32_t num_classes, int32_t 
         std::lock_guard<std::mutex> g(g_mu);
         p = plan_for(engine(c), B, H, W, input_u8 != 0);
     })
+    // zero first: every buffer starts from zero, as the Python host's arena does
+    EDGEDET_CHECK_HIP(hipMemsetAsync(workspace, 0, (size_t)p->arena, (hipStream_t)stream));
     for (auto& kv : p->consts) {
         char* dst = (char*)workspace + p->bufs[(size_t)kv.first].off;
         EDGEDET_CHECK_HIP(hipMemcpyAsync(dst, kv.second.data(), kv.second.size(), hipMemcpyHostToDevice,

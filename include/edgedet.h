@@ -99,7 +99,7 @@ int edgedet_graph_destroy(void* graph);
  * the device once.  Images: B x [3, H, W], float in [0, 1] (input_u8 = 0, detect.py:58) or the
  * decoded uint8 bytes (input_u8 = 1, divided by 255 on the device, bit-identical).  Workspace:
  * caller-owned device memory of edgedet_model_workspace_size bytes for (B, H, W, input_u8), set up
- * once by edgedet_model_prepare (writes the anchors / rescale constants; synchronous).  Outputs:
+ * once by edgedet_model_prepare (zeroes it and writes the anchors / rescale constants; synchronous).  Outputs:
  * count [B] int32, boxes [B][K][4] xyxy float in original pixels, scores [B][K] descending,
  * labels [B][K] int64, K = edgedet_model_max_detections(kind) (300 SSD / 100 FRCNN), the first
  * count[b] rows valid (detect.py:79-81).  forward is asynchronous on `stream`.
