@@ -136,8 +136,9 @@ CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads
     5: ("conv_mfma_kernel", 64, 64, 256), 6: ("conv_mfma_kernel", 32, 32, 64),
     10: ("pw_mfma_kernel", 256, 64, 256), 11: ("pw_mfma_kernel", 512, 32, 256), 12: ("pw_mfma_kernel", 128, 64, 256),
     15: ("pw_mfma_kernel", 256, 32, 256), 13: ("pw_splitk_kernel", 32, 32, 256), 14: ("pw_splitk_kernel", 32, 64, 256),
+    16: ("pw_splitk_kernel", 32, 32, 512), 17: ("pw_splitk_kernel", 32, 64, 512),
     21: ("conv_x6_kernel", 64, 64, 256), 22: ("conv_x6_kernel", 128, 64, 256), 23: ("conv_x6_kernel", 128, 128, 256), 24: ("conv_x6_kernel", 256, 128, 512),
-    25: ("conv_x6b_kernel", 256, 128, 512),
+    25: ("conv_x6b_kernel", 256, 128, 512), 27: ("conv_x6_kernel", 128, 64, 512), 28: ("conv_x6_kernel", 128, 128, 512),
 }
 
 

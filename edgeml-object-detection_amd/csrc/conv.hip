@@ -413,9 +413,9 @@ __global__ void __launch_bounds__(256) pw_mfma_kernel(ConvParams p) {
     conv_epilogue<TM, TN>(p, acc, m0, n0, h, l32);
 }
 
-template <int TN>
-__global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
-    __shared__ floatx16 red[3][TN][64];
+template <int TN, int NW>
+__global__ void __launch_bounds__(NW * 64) pw_splitk_kernel(ConvParams p) {
+    __shared__ floatx16 red[NW - 1][TN][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
     const int nnt = (p.Cout + 32 * TN - 1) / (32 * TN);
@@ -436,9 +436,9 @@ __global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
     const int nk = p.Kpad / 32;
     PwFrag<1, TN> cur, nxt;
     if (w < nk) pw_load<1, TN>(p, nxt, arow, ab, aval, brow, bval, w * 32 + 16 * h);
-    for (int ks = w; ks < nk; ks += 4) {
+    for (int ks = w; ks < nk; ks += NW) {
         cur = nxt;
-        if (ks + 4 < nk) pw_load<1, TN>(p, nxt, arow, ab, aval, brow, bval, (ks + 4) * 32 + 16 * h);
+        if (ks + NW < nk) pw_load<1, TN>(p, nxt, arow, ab, aval, brow, bval, (ks + NW) * 32 + 16 * h);
         pw_mma<1, TN>(cur, acc);
     }
     if (w > 0)
@@ -448,9 +448,13 @@ __global__ void __launch_bounds__(256) pw_splitk_kernel(ConvParams p) {
     if (w != 0) return;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const floatx16 r0 = red[0][j][lane], r1 = red[1][j][lane], r2 = red[2][j][lane];
+        floatx16 t = acc[0][j];
+        for (int q = 0; q < NW - 1; ++q) {  // fixed wave order
+            const floatx16 r = red[q][j][lane];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[0][j][r] = ((acc[0][j][r] + r0[r]) + r1[r]) + r2[r];
+            for (int e = 0; e < 16; ++e) t[e] += r[e];
+        }
+        acc[0][j] = t;
     }
     conv_epilogue<1, TN>(p, acc, m0, n0, h, l32);
 }
@@ -1173,11 +1177,11 @@ static int launch_pw(const ConvParams& p, hipStream_t s) {
     return 0;
 }
 
-template <int TN>
+template <int TN, int NW = 4>
 static int launch_pw_splitk(const ConvParams& p, hipStream_t s) {
     const int64_t nwg = cdiv(p.M, 32) * cdiv(p.Cout, 32 * TN);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "pw conv grid too large");
-    hipLaunchKernelGGL((pw_splitk_kernel<TN>), dim3((unsigned)nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((pw_splitk_kernel<TN, NW>), dim3((unsigned)nwg), dim3(NW * 64), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -1270,6 +1274,8 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 23: return launch_x6<2, 2, 2, 2>(p, s);  // 128 x 128, bf16x6
         case 24: return launch_x6<4, 2, 2, 2>(p, s);  // 256 x 128, bf16x6
         case 25: return launch_x6b(p, s);             // 256 x 128, bf16x6, 32-deep swizzled stages
+        case 27: return launch_x6<4, 2, 1, 1>(p, s);  // 128 x 64, bf16x6, 8 waves (32 x 32 each)
+        case 28: return launch_x6<4, 2, 1, 2>(p, s);  // 128 x 128, bf16x6, 8 waves (32 x 64 each)
         case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
             ConvParams q = p;
             q.ksplit = 2;
@@ -1296,6 +1302,12 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 13:
             EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
             return launch_pw_splitk<1>(p, s);           // split-K over 4 waves, 32 x 32
+        case 16:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw_splitk<1, 8>(p, s);        // split-K over 8 waves, 32 x 32
+        case 17:
+            EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
+            return launch_pw_splitk<2, 8>(p, s);        // split-K over 8 waves, 32 x 64
         case 14:
             EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
             return launch_pw_splitk<2>(p, s);           // split-K over 4 waves, 32 x 64

@@ -69,7 +69,7 @@ def test_conv_every_lds_tile(case, tile):
     _conv_case(*case, tile=tile)
 
 
-@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("case", [(2, 20, 20, 112, 672, 1, 1, "HS", False), (3, 10, 10, 40, 120, 1, 1, None, True),
                                   (2, 33, 31, 24, 72, 1, 1, "RE", False), (1, 9, 9, 16, 16, 1, 1, None, True),
                                   (2, 13, 11, 96, 24, 1, 1, "R6", False), (2, 20, 20, 672, 24, 1, 1, None, False),
@@ -272,7 +272,7 @@ def test_split_bf16x3_device_matches_host():
     assert np.array_equal(got, split_bf16x3(w.numpy()))
 
 
-@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25])
+@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25, 27, 28])
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 7, 8)])
 def test_conv_bf16x6_matches_torch(case, tile):
     _conv_case(*case, tile=tile, x6=True)

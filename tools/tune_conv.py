@@ -21,7 +21,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CANDIDATES = (1, 2, 3, 4, 5, 6, 10, 11, 12, 13, 14, 15, 21, 22, 23, 24, 25, 26)
+CANDIDATES = (1, 2, 3, 4, 5, 6, 10, 11, 12, 13, 14, 15, 16, 17, 21, 22, 23, 24, 25, 26, 27, 28)
 
 
 def time_record(L, O, rec, stream, reps):
@@ -39,7 +39,7 @@ def time_record(L, O, rec, stream, reps):
     return e0.elapsed_time(e1) / reps
 
 
-def tune_plan(plan, table, stream, log):
+def tune_plan(plan, table, stream, log, done):
     from edgeml_amd import ops as O
     from edgeml_amd.plan import conv_key
     L = O.lib()
@@ -51,8 +51,9 @@ def tune_plan(plan, table, stream, log):
         if op.kind != O.CONV:
             continue
         key = conv_key(op)
-        if key in table:
+        if key in done:
             continue
+        done.add(key)
         base = recs[k:k + 1].copy()
         base["i"][0, 23] = 0
         t0 = time_record(L, O, base, stream, 3)
@@ -83,7 +84,11 @@ def main():
     a = ap.parse_args()
     from edgeml_amd import models, plan as plan_mod
     plan_mod.CONV_TILES.clear()  # measure the library's own choice as "auto"
-    table, log = {}, []
+    # re-tune the shapes of the given models, keep the other entries of the existing table
+    table, log, done = {}, [], set()
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            table.update(json.load(f).get("tiles", {}))
     stream = torch.cuda.Stream()
     for name in a.models.split(","):
         if name == "ssd":
@@ -98,7 +103,7 @@ def main():
         for B, H, W in shapes:
             print(f"== {name} B={B} {H}x{W}", flush=True)
             p = m.plan(B, H, W)
-            tune_plan(p, table, stream, log)
+            tune_plan(p, table, stream, log, done)
             m.plans.clear()
             del p
             torch.cuda.empty_cache()
