@@ -21,6 +21,9 @@
 //                  fused MBConv front when p5 != 0: p0 is the block input [B,H,W,i11 Cin], p5 the
 //                  1x1 expansion weight [C][i12 ld], p6 its bias, i13 its activation
 //                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16)
+//   MBCONV         InvertedResidual without SE in one kernel: p0 x; p1 expand w [Cexp][i12]; p2 b1;
+//                  p3 dw w [K*K][Cexp]; p4 bd; p5 project w [Cout][i13]; p6 b2; p7 y;
+//                  i0..11 B,H,W,Cin,Cexp,Cout,Ho,Wo,K,stride,pad,act; i14 residual
 //   CHANNEL_MEAN   p0 x[B,HW,C]; p1 mean[B,C]; i0..2 B,HW,C
 //   SE_FC          p0 part[B,16,C]; p1 w1[S][C]; p2 b1; p3 w2t[S][C]; p4 b2; p5 scale[B,C]; p6 hidden[B,S];
 //                  i0..4 B,C,S,HW,splits (0 = 16)
@@ -144,6 +147,33 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
                 p.stdv[c] = o.f[3 + c];
             }
             return preprocess_launch(p, s);
+        }
+        case EDGEDET_OP_MBCONV: {
+            MbParams p{};
+            p.x = P<const float>(o, 0);
+            p.w1 = P<const float>(o, 1);
+            p.b1 = P<const float>(o, 2);
+            p.wd = P<const float>(o, 3);
+            p.bd = P<const float>(o, 4);
+            p.w2 = P<const float>(o, 5);
+            p.b2 = P<const float>(o, 6);
+            p.y = P<float>(o, 7);
+            p.B = (int)I[0];
+            p.H = (int)I[1];
+            p.W = (int)I[2];
+            p.Cin = (int)I[3];
+            p.Cexp = (int)I[4];
+            p.Cout = (int)I[5];
+            p.Ho = (int)I[6];
+            p.Wo = (int)I[7];
+            p.K = (int)I[8];
+            p.stride = (int)I[9];
+            p.pad = (int)I[10];
+            p.act = (int)I[11];
+            p.ld1 = (int)I[12];
+            p.ld2 = (int)I[13];
+            p.residual = (int)I[14];
+            return mbconv_launch(p, s);
         }
         case EDGEDET_OP_CONV: {
             const ConvParams p = conv_params(o);

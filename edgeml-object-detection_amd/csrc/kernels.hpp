@@ -52,6 +52,20 @@ struct DwParams {
     int Cin, w1_ld, act1;
 };
 
+// A whole InvertedResidual without SqueezeExcitation (csrc/layers.hip mbconv_kernel).
+struct MbParams {
+    const float* x;   // [B][H][W][Cin] the block input (dense NHWC)
+    const float* w1;  // expand [Cexp][ld1] (packed 1x1 weight, folded BN)
+    const float* b1;  // [Cexp]
+    const float* wd;  // depthwise [K*K][Cexp]
+    const float* bd;  // [Cexp]
+    const float* w2;  // project [Cout][ld2]
+    const float* b2;  // [Cout]
+    float* y;         // [B][Ho][Wo][Cout]
+    int B, H, W, Cin, Cexp, Cout, Ho, Wo, K, stride, pad, act, ld1, ld2, residual;
+};
+int mbconv_launch(const MbParams& p, hipStream_t s);
+
 struct PoolParams {
     const float* x;
     float* y;

@@ -564,6 +564,195 @@ static int mbconv_front_launch(const DwParams& p, hipStream_t s) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------ fused MBConv
+// A whole torchvision InvertedResidual without SqueezeExcitation (the SSDLite
+// backbone's high-resolution blocks 0.2 and 0.3): expand 1x1 (+ folded BN, act), depthwise KxK
+// stride S (+ folded BN, act), project 1x1 (+ folded BN), + the block input when S == 1 and
+// Cin == Cout.  Neither the 3-4x-wide expanded tensor nor the depthwise output reaches HBM: per
+// block (one image, an 8 x 8 output tile) the input halo ((8-1)*S + K)^2 x Cin is read once, and
+// the expanded channels are processed in chunks of 32 through LDS:
+//   expand   lane = one expanded channel of the chunk (its weight row in registers), a wave covers
+//            two halo pixels per step (broadcast LDS reads of the input row); halo pixels outside
+//            the image are zero (the depthwise pads the expanded tensor);
+//   depthwise taps in (kh, kw) order, as dw_group;
+//   project  partial sums over the chunk added in chunk order into registers (output pixel x
+//            output channel per thread), so the sum runs over the expanded channels in order.
+// All arithmetic is fp32 fmaf in the reference op order ((sum + bias) -> act; (sum + bias) + residual).
+// Measured 3.5-4.5x slower than the three separate ops on SSDLite blocks 0.2 / 0.3 (255 / 260 us
+// against 74 / 58 us per 16-image chain: at two blocks per CU each block's dependent phases leave its
+// LDS reads and VALU chains exposed, PMC: ~16 cycles per issued instruction), so the lowering keeps
+// the separate ops unless EDGEDET_MB_BLOCK=1.
+constexpr int MBF_T = 8, MBF_CC = 32, MBF_MAXCIN = 32, MBF_MAXCOUT = 32;
+
+template <int K, int S, int CINB>
+struct MbfGeom {
+    static constexpr int IH = (MBF_T - 1) * S + K, IP = IH * IH;
+    static constexpr int XS = CINB + 1, ES = MBF_CC + 1;
+};
+
+// CINB: the input-channel bound the block is compiled for (16 or 32; LDS rows and weight registers)
+template <int K, int S, int ACT, int CINB>
+__global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
+    using G = MbfGeom<K, S, CINB>;
+    constexpr int IH = G::IH, IP = G::IP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
+    constexpr int NOUT = (TT * MBF_MAXCOUT + 255) / 256;  // output items per thread
+    __shared__ float xs[IP * XS];  // input halo [pixel][Cin]
+    __shared__ float es[IP * ES];  // expanded chunk [halo pixel][32]
+    __shared__ float ds[TT * ES];  // depthwise chunk [output pixel][32]
+    __shared__ float w2s[MBF_MAXCOUT * ES];  // project weights of the chunk [co][32] (zero past Cexp)
+    const int tid = threadIdx.x, b = blockIdx.y;
+    const int oh0 = (blockIdx.x / tiles_w) * MBF_T, ow0 = (blockIdx.x % tiles_w) * MBF_T;
+    const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
+    const int Cin = p.Cin, Cexp = p.Cexp, Cout = p.Cout;
+    const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
+    // 1. input halo, all of a thread's loads in flight together
+    {
+        constexpr int MAXN = (IP * CINB + 255) / 256;
+        const int n = IP * Cin;
+        float v[MAXN];
+#pragma unroll
+        for (int r = 0; r < MAXN; ++r) {
+            const int t = tid + 256 * r;
+            const int px = t / Cin, c = t - px * Cin;
+            const int ih = ih0 + px / IH, iw = iw0 + px % IH;
+            const bool in = t < n && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            v[r] = in ? xb[((int64_t)ih * p.W + iw) * Cin + c] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < MAXN; ++r) {
+            const int t = tid + 256 * r;
+            if (t < n) {
+                const int px = t / Cin;
+                xs[px * XS + (t - px * Cin)] = v[r];
+            }
+        }
+    }
+    float acc[NOUT];
+#pragma unroll
+    for (int r = 0; r < NOUT; ++r) acc[r] = 0.f;
+    const int cl = tid & (MBF_CC - 1), pg = tid >> 5;  // chunk channel, pixel group (8 groups)
+    for (int c0 = 0; c0 < Cexp; c0 += MBF_CC) {
+        const int ce = c0 + cl;
+        const bool cok = ce < Cexp;
+        // 2. expand: channel ce of the halo pixels pg, pg + 8, ...
+        float w[CINB];
+#pragma unroll
+        for (int i = 0; i < CINB; ++i) w[i] = (cok && i < Cin) ? p.w1[(int64_t)ce * p.ld1 + i] : 0.f;
+        const float be = cok ? p.b1[ce] : 0.f;
+        constexpr int W2N = (MBF_MAXCOUT * MBF_CC + 255) / 256;
+        float w2v[W2N];
+#pragma unroll
+        for (int r = 0; r < W2N; ++r) {  // loads in flight across the expansion
+            const int t = tid + 256 * r, co = t / MBF_CC, j = t % MBF_CC;
+            w2v[r] = (co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
+        }
+        __syncthreads();  // xs written / the previous chunk's es, ds and w2s consumed
+        for (int px = pg; px < IP; px += 8) {
+            const int ih = ih0 + px / IH, iw = iw0 + px % IH;
+            const float* xr = xs + px * XS;
+            float a = 0.f;
+#pragma unroll
+            for (int i = 0; i < CINB; ++i)
+                if (i < Cin) a = fmaf(w[i], xr[i], a);
+            const bool in = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            es[px * ES + cl] = in ? apply_act(a + be, ACT) : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < W2N; ++r) {
+            const int t = tid + 256 * r;
+            w2s[(t / MBF_CC) * ES + t % MBF_CC] = w2v[r];
+        }
+        __syncthreads();
+        // 3. depthwise on the 8 x 8 output pixels (pixel groups of 8), taps in (kh, kw) order
+        {
+            float wt[K * K];
+#pragma unroll
+            for (int t = 0; t < K * K; ++t) wt[t] = cok ? p.wd[t * Cexp + ce] : 0.f;
+            const float bdv = cok ? p.bd[ce] : 0.f;
+            for (int op = pg; op < TT; op += 8) {
+                const int lh = op / MBF_T, lw = op % MBF_T;
+                const int oh = oh0 + lh;
+                float a = 0.f;
+#pragma unroll
+                for (int kh = 0; kh < K; ++kh) {
+                    if ((unsigned)(oh * S - p.pad + kh) >= (unsigned)p.H) continue;  // as dw_group: rows off the map
+#pragma unroll
+                    for (int kw = 0; kw < K; ++kw) {
+                        const int iw = (ow0 + lw) * S - p.pad + kw;
+                        if ((unsigned)iw >= (unsigned)p.W) continue;
+                        a = fmaf(es[((lh * S + kh) * IH + lw * S + kw) * ES + cl], wt[kh * K + kw], a);
+                    }
+                }
+                ds[op * ES + cl] = apply_act(a + bdv, ACT);
+            }
+        }
+        __syncthreads();
+        // 4. project: this chunk's partial sums, channel order (channels past Cexp: zero weight and
+        //    zero depthwise value, adding +0)
+#pragma unroll
+        for (int r = 0; r < NOUT; ++r) {
+            const int it = tid + 256 * r;
+            if (it < TT * Cout) {
+                const int op = it / Cout, co = it - op * Cout;
+                const float* dr = ds + op * ES;
+                const float* wr = w2s + co * ES;
+                float a = acc[r];
+#pragma unroll
+                for (int j = 0; j < MBF_CC; ++j) a = fmaf(wr[j], dr[j], a);
+                acc[r] = a;
+            }
+        }
+    }
+    // 5. bias, residual, store
+#pragma unroll
+    for (int r = 0; r < NOUT; ++r) {
+        const int it = tid + 256 * r;
+        if (it < TT * Cout) {
+            const int op = it / Cout, co = it - op * Cout;
+            const int lh = op / MBF_T, lw = op % MBF_T, oh = oh0 + lh, ow = ow0 + lw;
+            if (oh < p.Ho && ow < p.Wo) {
+                float v = acc[r] + p.b2[co];
+                if (p.residual) v = v + xs[((lh + p.pad) * IH + lw + p.pad) * XS + co];  // S == 1: the input pixel
+                p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
+            }
+        }
+    }
+}
+
+template <int K, int S, int CINB>
+static int mbconv_launch_ksc(const MbParams& p, hipStream_t s) {
+    const int tiles_w = cdiv(p.Wo, MBF_T);
+    const dim3 grid((unsigned)(cdiv(p.Ho, MBF_T) * tiles_w), (unsigned)p.B);
+    switch (p.act) {
+        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
+        default: EDGEDET_REQUIRE(false, "mbconv: activation RE / R6 / HS");
+    }
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int K, int S>
+static int mbconv_launch_ks(const MbParams& p, hipStream_t s) {
+    return p.Cin <= 16 ? mbconv_launch_ksc<K, S, 16>(p, s) : mbconv_launch_ksc<K, S, 32>(p, s);
+}
+
+int mbconv_launch(const MbParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.x && p.w1 && p.b1 && p.wd && p.bd && p.w2 && p.b2 && p.y, "mbconv: null pointer");
+    EDGEDET_REQUIRE(p.Cin >= 1 && p.Cin <= MBF_MAXCIN && p.Cout >= 1 && p.Cout <= MBF_MAXCOUT && p.Cexp >= 1,
+                    "mbconv: Cin, Cout <= 32");
+    EDGEDET_REQUIRE(p.ld1 >= p.Cin && p.ld2 >= p.Cexp, "mbconv: weight row strides");
+    EDGEDET_REQUIRE(p.pad == (p.K - 1) / 2 && p.Ho == (p.H + 2 * p.pad - p.K) / p.stride + 1 &&
+                    p.Wo == (p.W + 2 * p.pad - p.K) / p.stride + 1, "mbconv: 'same' padding shape");
+    EDGEDET_REQUIRE(!p.residual || (p.stride == 1 && p.Cin == p.Cout), "mbconv: residual needs stride 1, Cin == Cout");
+    if (p.K == 3 && p.stride == 1) return mbconv_launch_ks<3, 1>(p, s);
+    if (p.K == 3 && p.stride == 2) return mbconv_launch_ks<3, 2>(p, s);
+    if (p.K == 5 && p.stride == 1) return mbconv_launch_ks<5, 1>(p, s);
+    if (p.K == 5 && p.stride == 2) return mbconv_launch_ks<5, 2>(p, s);
+    EDGEDET_REQUIRE(false, "mbconv: K in {3, 5}, stride in {1, 2}");
+}
+
 // LDS bytes the fused front needs (0 = shape not supported); the plan uses it to decide fusion.
 extern "C" int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin) {
     if (K == 3 && stride == 1) return (int64_t)MbGeom<3, 1>::lds_bytes(Cin);

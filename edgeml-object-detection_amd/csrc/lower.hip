@@ -670,8 +670,35 @@ class SSDLite {
             P.add(o);
             return P.ref(scale);
         };
+        auto mb_block = [&](const Cur& in, const Block& b, const Prefixes& pf) {
+            ConvW w1 = cbn(pf.pe, b.exp, b.cin, 1, false);
+            ConvW wd = cbn(pf.pd, b.exp, b.exp, b.k, true);
+            ConvW w2 = cbn(pf.pp, b.cout, b.exp, 1, false);
+            const int pad = (b.k - 1) / 2;
+            const int64_t Ho = (in.s[1] + 2 * pad - b.k) / b.stride + 1, Wo = (in.s[2] + 2 * pad - b.k) / b.stride + 1;
+            std::vector<int64_t> ys = {B, Ho, Wo, b.cout};
+            const int y = P.buf(ys, 4, pf.pp + sfx);
+            OpRec o;
+            o.kind = EDGEDET_OP_MBCONV;
+            const int64_t iv[15] = {B, in.s[1], in.s[2], b.cin, b.exp, b.cout, Ho, Wo, b.k, b.stride, pad, b.act,
+                                    w1.Kpad, w2.Kpad, (b.stride == 1 && b.cin == b.cout) ? 1 : 0};
+            for (int j = 0; j < 15; ++j) o.i[j] = iv[j];
+            o.p[0] = in.x;
+            o.p[1] = Plan::wref(w1.w);
+            o.p[2] = Plan::wref(w1.b);
+            o.p[3] = Plan::wref(wd.w);
+            o.p[4] = Plan::wref(wd.b);
+            o.p[5] = Plan::wref(w2.w);
+            o.p[6] = Plan::wref(w2.b);
+            o.p[7] = P.ref(y);
+            P.add(o);
+            return Cur{P.ref(y), ys};
+        };
         auto inverted_residual = [&](const Cur& in, const Block& b, const std::string& base) {
             Prefixes pf = block_prefixes(b, base);
+            if (env_int("EDGEDET_MB_BLOCK", 0) == 1 && !pack_only && !pf.pe.empty() && !b.se && b.cin <= 32 &&
+                b.cout <= 32)
+                return mb_block(in, b, pf);
             Cur y = in;
             if (!pf.pe.empty()) y = conv(y, pf.pe, b.exp, 1, 1, b.act);
             DwOut d = dw(y, pf.pd, b.k, b.stride, b.act, b.se);

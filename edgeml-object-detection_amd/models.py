@@ -24,6 +24,11 @@ from .plan import BufView, Op, Plan, WeightPack, conv_op, fold_bn, pack_conv_wei
 # tensor kept in LDS.  Off by default: measured slower than the two ops (csrc/layers.hip
 # mbconv_front_kernel header); EDGEDET_MBCONV_FUSE=1 selects it.
 MBCONV_FUSE = os.environ.get("EDGEDET_MBCONV_FUSE", "0") == "1"
+# A whole InvertedResidual without SE (expand, depthwise, project, residual) as one kernel where its
+# input and output are at most 32 channels wide (SSDLite blocks 0.2 and 0.3, csrc/layers.hip
+# mbconv_kernel).  Opt-in (EDGEDET_MB_BLOCK=1): correct, but measured 3.5-4.5x slower than the three
+# separate ops (0.2: 255 vs 74 us per 16-image chain, 0.3: 260 vs 58 us; SSD 17.0k vs 25.2k img/s).
+MB_BLOCK_FUSE = os.environ.get("EDGEDET_MB_BLOCK", "0") == "1"
 # SSDLite features.0.0 + features.0.1 as one kernel (csrc/layers.hip ssd_stem_kernel); =0 lowers the
 # three separate ops.
 SSD_STEM_FUSE = os.environ.get("EDGEDET_SSD_STEM_FUSE", "1") == "1"
@@ -428,9 +433,32 @@ class SSDLite320(_Detector):
                      {0: xb, 1: w, 2: b, 3: y, 4: None, 5: w1, 6: b1}, name=pe + "+" + pd.rsplit(".", 1)[-1]))
             return (y, ys)
 
+        def mb_block(cur, cnf, pe, pd, pp):
+            """The whole block as one MBCONV op (csrc/layers.hip mbconv_kernel)."""
+            xb, xs = cur
+            cin, k, exp, cout, use_se, act, stride = cnf
+            w1, b1, _, kpad1, _ = self._conv_bn(pe + ".0.weight", pe + ".1", self.BN_EPS)
+            wd, bd, _, _, _ = self._conv_bn(pd + ".0.weight", pd + ".1", self.BN_EPS)
+            w2, b2, _, kpad2, _ = self._conv_bn(pp + ".0.weight", pp + ".1", self.BN_EPS)
+            pad = (k - 1) // 2
+            Ho = (xs[1] + 2 * pad - k) // stride + 1
+            Wo = (xs[2] + 2 * pad - k) // stride + 1
+            ys = (B, Ho, Wo, cout)
+            y = P.buf(ys, name=pp + sfx)
+            P.add(Op(ops.MBCONV, {0: B, 1: xs[1], 2: xs[2], 3: cin, 4: exp, 5: cout, 6: Ho, 7: Wo, 8: k, 9: stride,
+                                  10: pad, 11: ops.ACT[act], 12: kpad1, 13: kpad2,
+                                  14: int(stride == 1 and cin == cout)},
+                     {0: xb, 1: w1, 2: b1, 3: wd, 4: bd, 5: w2, 6: b2, 7: y}, name=base_name(pe)))
+            return (y, ys)
+
+        def base_name(pe):
+            return pe.rsplit(".", 1)[0]
+
         def inverted_residual(cur, cnf, base):
             cin, k, exp, cout, use_se, act, stride = cnf
             pe, pd, ps, pp = arch.block_prefixes(cnf, base)
+            if MB_BLOCK_FUSE and not pack_only and pe and not use_se and cin <= 32 and cout <= 32:
+                return mb_block(cur, cnf, pe, pd, pp)
             y = cur
             fused = mbfront(y, pe, pd, k, stride, act) if pe and not use_se and not pack_only else None
             if fused is not None:

@@ -22,6 +22,7 @@ SSD_SCORES, SSD_CLASS_NMS, MERGE_TOPK, RPN_LEVEL_NMS, ROI_ALIGN, BOX_SCORES, BOX
 FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
 GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 SSD_STEM = 21
+MBCONV = 22
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)

@@ -67,7 +67,8 @@ enum {
     EDGEDET_OP_GN_STATS = 18,     /* GroupNorm statistics -> per (image, channel) scale / shift       */
     EDGEDET_OP_RETINA_SELECT = 19,/* RetinaNet per (image, level): sigmoid > t, top-k, decode, clip   */
     EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
-    EDGEDET_OP_SSD_STEM = 21      /* SSDLite features.0.0 + features.0.1 in one pass                  */
+    EDGEDET_OP_SSD_STEM = 21,     /* SSDLite features.0.0 + features.0.1 in one pass                  */
+    EDGEDET_OP_MBCONV = 22        /* InvertedResidual without SE: expand, depthwise, project, residual */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,

@@ -351,3 +351,52 @@ def test_conv_bf16x6_is_fp32_grade(shape):
             errs[f"{name}{tile}"] = (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max().item()
     assert errs["x623"] <= 1.5 * errs["f323"] + 1e-7, errs
     assert errs["x625"] <= 1.5 * errs["f323"] + 1e-7, errs
+
+
+@pytest.mark.parametrize("B,H,W,Cin,E,Cout,k,s,act", [
+    (2, 160, 160, 16, 64, 24, 3, 2, "RE"),    # SSDLite block 0.2
+    (3, 80, 80, 24, 72, 24, 3, 1, "RE"),      # block 0.3 (residual)
+    (1, 37, 29, 12, 40, 20, 5, 2, "HS"),      # ragged tiles, K = 5, a partial channel chunk
+    (2, 9, 11, 32, 96, 32, 5, 1, "R6"),       # residual with the 32-channel bound
+])
+def test_mbconv_block_matches_torch(B, H, W, Cin, E, Cout, k, s, act):
+    """The whole InvertedResidual in one kernel (MBCONV record: expand 1x1 + act, depthwise + act,
+    project 1x1, + residual when stride 1 and Cin == Cout) against torch fp32."""
+    import ctypes
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight, pack_dw_weight
+    g = torch.Generator().manual_seed(B * 1000 + H + E)
+    x = torch.randn(B, H, W, Cin, generator=g)
+    w1 = torch.randn(E, Cin, 1, 1, generator=g) / Cin ** 0.5
+    b1 = torch.randn(E, generator=g) * 0.1
+    wd = torch.randn(E, 1, k, k, generator=g) / k
+    bd = torch.randn(E, generator=g) * 0.1
+    w2 = torch.randn(Cout, E, 1, 1, generator=g) / E ** 0.5
+    b2 = torch.randn(Cout, generator=g) * 0.1
+    pad = (k - 1) // 2
+    xc = x.permute(0, 3, 1, 2).double()
+    e = _act(F.conv2d(xc, w1.double(), b1.double()), act)
+    d = _act(F.conv2d(e, wd.double(), bd.double(), stride=s, padding=pad, groups=E), act)
+    y = F.conv2d(d, w2.double(), b2.double())
+    res = s == 1 and Cin == Cout
+    if res:
+        y = y + xc
+    ref = y.permute(0, 2, 3, 1).float()
+    Ho, Wo = ref.shape[1], ref.shape[2]
+    p1, _, kp1, _ = pack_conv_weight(w1.numpy())
+    p2, _, kp2, _ = pack_conv_weight(w2.numpy())
+    dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (p1, b1.numpy(), pack_dw_weight(wd.numpy()),
+                                                                     bd.numpy(), p2, b2.numpy())]
+    xd = x.cuda()
+    yd = torch.full((B, Ho, Wo, Cout), float("nan"), device="cuda")
+    rec = np.zeros(1, dtype=ops.OP_DTYPE)
+    rec[0]["kind"] = ops.MBCONV
+    for j, v in enumerate((B, H, W, Cin, E, Cout, Ho, Wo, k, s, pad, ops.ACT[act], kp1, kp2, int(res))):
+        rec[0]["i"][j] = v
+    for j, t in enumerate([xd] + dev + [yd]):
+        rec[0]["p"][j] = t.data_ptr()
+    ops.check(ops.lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, ops.stream_handle()))
+    torch.cuda.synchronize()
+    got = yd.cpu()
+    err = (got - ref).abs().max().item()
+    assert torch.isfinite(got).all() and err <= 1e-4 * max(1.0, ref.abs().max().item()), err

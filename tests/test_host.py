@@ -159,8 +159,12 @@ def test_ssd_plan_lowering():
     n_dw = kinds.count(ops.DWCONV)
     stem = kinds.count(ops.SSD_STEM)
     assert stem == (1 if models.SSD_STEM_FUSE else 0)
-    assert n_dw == 15 + 4 + 12 - stem
-    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12 - 2 * stem
+    # blocks 0.2 and 0.3 (no SE, <= 32 channels in and out) as single MBCONV ops: one depthwise and
+    # two convs fewer each
+    mb = kinds.count(ops.MBCONV)
+    assert mb == (2 if models.MB_BLOCK_FUSE else 0)
+    assert n_dw == 15 + 4 + 12 - stem - mb
+    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12 - 2 * stem - 2 * mb
     assert kinds.count(ops.SE_FC) == 8
     assert m.grids == [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
     for op in P.ops:
