@@ -75,3 +75,17 @@ def test_pack_rejects_bad_state_dict(built):
     bad["backbone.features.0.0.0.weight"] = torch.zeros(16, 3, 3, 2)
     with pytest.raises(ops.EdgeDetError, match="size mismatch"):
         native.pack_state_dict("ssd", bad, 91, True)
+
+
+def test_records_identical_with_fused_blocks(built, monkeypatch):
+    """The opt-in whole-block MBCONV lowering (EDGEDET_MB_BLOCK=1) is mirrored by the native host."""
+    sd, m = built("ssd", 91, True)
+    monkeypatch.setattr(models, "MB_BLOCK_FUSE", True)
+    monkeypatch.setenv("EDGEDET_MB_BLOCK", "1")
+    B, H, W = 5, 300, 400  # a shape no other test lowers (the native host caches plans per shape)
+    P = _python_plan(m, B, H, W, False)
+    assert sum(op.kind == ops.MBCONV for op in P.ops) == 2
+    rec = native.records("ssd", B, H, W, P.weights.device_blob.data_ptr(), P.arena.data_ptr(), 91, True, False)
+    assert len(rec) == len(P.records)
+    for k, (a, b) in enumerate(zip(rec, P.records)):
+        assert a.tobytes() == b.tobytes(), (k, P.ops[k].name)
