@@ -740,6 +740,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 #ifndef X6B_PIPE
 #define X6B_PIPE 1
 #endif
+#ifndef X6B_STAGGER
+#define X6B_STAGGER 0
+#endif
 #ifndef X6B_GLDS
 #define X6B_GLDS 1
 #endif
@@ -836,8 +839,9 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int64_t x3plane = (int64_t)p.B * p.H * p.W * p.Cin;
     // x3 scratch: X3Z zero elements (the source of padding taps under LDS-DMA), then the three planes
     const unsigned short* x3 = reinterpret_cast<const unsigned short*>(p.x3);
-    auto load_stage = [&](Regs& R, int k0, int bbuf) {
-        if constexpr (GL) {
+    // la / lb: load the stage's A rows (to registers, or to LDS by DMA under PS && GL) / its B rows
+    auto load_part = [&](Regs& R, int k0, int bbuf, bool la, bool lb) {
+        if (GL && lb) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
             // -> the 16-B slot l of the block); the swizzle is applied on the source address
             const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 2) & 3);
@@ -849,7 +853,8 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
                     (const __attribute__((address_space(1))) void*)(src + pl * wplane),
                     (__attribute__((address_space(3))) void*)(Bs + bbuf * 3 * PB + pl * PB + 16 * wid * BK6B), 16, 0, 0);
         }
-        if constexpr (PS) {
+        if (!la) {
+        } else if constexpr (PS) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
             const int kw = tap - kh * p.KW;
@@ -916,12 +921,13 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
                 R.a[j] = v;
             }
         }
-        if constexpr (!GL) {
+        if (!GL && lb) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
                 R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
         }
     };
+    auto load_stage = [&](Regs& R, int k0, int bbuf) { load_part(R, k0, bbuf, true, true); };
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
@@ -963,7 +969,31 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     const int nk_all = p.Kpad / BK6B;
     const int kbeg = ksp > 1 ? (blockIdx.x & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
     const int nk = ksp > 1 ? ((blockIdx.x & 1) ? nk_all - kbeg : (nk_all + 1) / 2) : nk_all;
-    const int kofs = kbeg * BK6B;
+    // Stage order. Tap-major (stage s at k = 32 s, the weight layout) sweeps a block's whole input
+    // panel once per filter tap; with p.korder and a uniform tap the stages run channel-chunk-major
+    // instead (the KH*KW taps of one 32-channel chunk back to back, k = tap * Cin + 32 * chunk), so
+    // the chunk's input window is re-read from L2 across the taps rather than from HBM.  Stages are
+    // loaded strictly in order, so the position advances by one per load.
+    const bool cm = UT && p.korder && KHW > 1 && p.Kpad == KHW * p.Cin;
+    struct Cursor {
+        int tap, chunk, k;
+    };
+    Cursor ca{cm ? kbeg % KHW : 0, cm ? kbeg / KHW : 0, kbeg * BK6B};
+    auto next_k = [&](Cursor& c) {
+        int k0;
+        if (cm) {
+            k0 = c.tap * p.Cin + c.chunk * BK6B;
+            if (++c.tap == KHW) {
+                c.tap = 0;
+                ++c.chunk;
+            }
+        } else {
+            k0 = c.k;
+            c.k += BK6B;
+        }
+        return k0;
+    };
+    Cursor cb = ca;  // the B rows' cursor (runs behind ca in the late wave group of the stagger)
     const int h = lane >> 5;
     const int l32 = lane & 31;
     struct Frags {
@@ -1013,23 +1043,58 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // barrier) runs while stage k's first-half fragments are read, and stage k+1's operands are
     // written to the other buffer under stage k's MFMAs, so the matrix pipe does not idle through
     // the read latency after each barrier.
+#if X6B_STAGGER
+    // Stagger: the two waves that share a SIMD (w and w + 4) would otherwise run in lockstep, both in
+    // their MFMAs and both in their split/stores at the same time.  Waves 4..7 store stage k+1 (A
+    // loaded one stage earlier, still a full stage of latency) at the start of stage k, then load
+    // stage k+2's A rows; waves 0..3 keep the load-early / store-late order.  Same LDS image and
+    // barriers, so results are unchanged.  Measured slower on every arrangement (box head 3x3, tile
+    // 25: 2.29 ms lockstep; 2.56 late-store group; 2.46 / 2.47 mid-store in waves 4..7 / 0..3), so
+    // off by default (X6B_STAGGER=0).
+    const bool upper = __builtin_amdgcn_readfirstlane(wid) >= 4;
+    const bool late = X6B_STAGGER == 1 && GL && !PS && upper;
+    // (2 / 3: waves 4..7 / 0..3 store between the two MFMA halves instead)
+    const bool mid = (X6B_STAGGER == 2 && upper) || (X6B_STAGGER == 3 && !upper);
+#else
+    const bool late = false, mid = false;
+#endif
     Regs r0;
     Frags F0, F1;
-    load_stage(r0, kofs, 0);
+    load_stage(r0, next_k(ca), 0);
+    (void)next_k(cb);
     store_stage(r0, 0);
+    if (late && nk > 1) load_part(r0, next_k(ca), 0, true, false);
     __syncthreads();
-    if (nk > 1) load_stage(r0, kofs + BK6B, 1);
+    if (nk > 1) {
+        if (late) {
+            load_part(r0, next_k(cb), 1, false, true);
+            store_stage(r0, 1);
+            if (nk > 2) load_part(r0, next_k(ca), 0, true, false);
+        } else {
+            load_stage(r0, next_k(ca), 1);
+            (void)next_k(cb);
+        }
+    }
     read_frags(F0, 0, 0);
     mfmas(F0);
     read_frags(F1, 0, 1);
-    if (nk > 1) store_stage(r0, 1);
+    if (!late && nk > 1) store_stage(r0, 1);
     __syncthreads();
     for (int kc = 1; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, kofs + (kc + 1) * BK6B, buf ^ 1);
+        if (late) {
+            if (kc + 1 < nk) {
+                load_part(r0, next_k(cb), buf ^ 1, false, true);
+                store_stage(r0, buf ^ 1);
+            }
+            if (kc + 2 < nk) load_part(r0, next_k(ca), buf ^ 1, true, false);
+        } else if (kc + 1 < nk) {
+            load_stage(r0, next_k(ca), buf ^ 1);
+        }
         read_frags(F0, buf, 0);
         __builtin_amdgcn_sched_barrier(0);  // issue the reads before the MFMAs that hide them
         mfmas(F1);
+        if (mid && kc + 1 < nk) store_stage(r0, buf ^ 1);
 #if X6B_PIPE == 2
         store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
         mfmas(F0);
@@ -1037,7 +1102,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
 #else
         mfmas(F0);
         read_frags(F1, buf, 1);
-        store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+        if (!late && !mid) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
 #endif
         __syncthreads();
     }
@@ -1047,12 +1112,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
     // time to land.
     Regs r0, r1;
-    load_stage(r0, kofs, 0);
+    load_stage(r0, next_k(ca), 0);
     store_stage(r0, 0);
-    if (nk > 1) load_stage(r1, kofs + BK6B, 1);
+    if (nk > 1) load_stage(r1, next_k(ca), 1);
     __syncthreads();
     auto step = [&](int kc, Regs& hold, Regs& next) {
-        if (kc + 2 < nk) load_stage(next, kofs + (kc + 2) * BK6B, kc & 1);  // (no LDS-DMA with two register stages)
+        if (kc + 2 < nk) load_stage(next, next_k(ca), kc & 1);  // (no LDS-DMA with two register stages)
         compute(kc & 1);
         if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
         __syncthreads();
@@ -1063,12 +1128,12 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     }
 #else
     Regs r0;
-    load_stage(r0, kofs, 0);
+    load_stage(r0, next_k(ca), 0);
     store_stage(r0, 0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, kofs + (kc + 1) * BK6B, buf ^ 1);
+        if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
         compute(buf);
         if (kc + 1 < nk) store_stage(r0, buf ^ 1);
         __syncthreads();
@@ -1113,7 +1178,19 @@ static bool x6b_presplit(const ConvParams& p) {
     return p.x3 && p.Cin % BK6B == 0 && p.x_pstride % 4 == 0 && ((uintptr_t)p.x3 & 15) == 0;
 }
 
-static int launch_x6b(const ConvParams& p, hipStream_t s) {
+// Channel-chunk-major K stages in conv_x6b_kernel (EDGEDET_X6B_KORDER=0: tap-major, the order of
+// the weight layout).  Changes the fp32 accumulation order, not the terms summed.
+static int x6b_korder() {
+    static const int v = [] {
+        const char* e = std::getenv("EDGEDET_X6B_KORDER");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
+static int launch_x6b(const ConvParams& p0, hipStream_t s) {
+    ConvParams p = p0;
+    p.korder = x6b_korder();
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
     EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
     if (p.ksplit > 1)

@@ -12,11 +12,12 @@ import build as B  # noqa: E402
 name, extra = sys.argv[1], sys.argv[2:]
 od = os.path.join(ROOT, "build", "variants", name)
 os.makedirs(od, exist_ok=True)
+B.write_tile_table(od)
 
 
 def cc(src):
     obj = os.path.join(od, os.path.basename(src)[:-4] + ".o")
-    r = subprocess.run([B.hipcc(), *B.FLAGS, *extra, "-c", src, "-o", obj], capture_output=True, text=True)
+    r = subprocess.run([B.hipcc(), *B.FLAGS, *extra, "-I", od, "-c", src, "-o", obj], capture_output=True, text=True)
     if r.returncode:
         raise SystemExit(r.stderr)
     return obj
