@@ -740,6 +740,12 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 #ifndef X6B_PIPE
 #define X6B_PIPE 1
 #endif
+#ifndef X6B_IGLP
+#define X6B_IGLP 3
+#endif
+#ifndef X6B_BRANCHLESS
+#define X6B_BRANCHLESS 0
+#endif
 #ifndef X6B_STAGGER
 #define X6B_STAGGER 0
 #endif
@@ -895,13 +901,22 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             const float* xt = p.x + (int64_t)(kh * p.W + kw) * p.x_pstride + ci;
 #pragma unroll
             for (int j = 0; j < AJ; ++j) {
+                // branch-free (a padding tap loads from p.x and is zeroed), so the stage is one
+                // basic block the scheduler can interleave
                 const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+                const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+#if X6B_BRANCHLESS
+                f32x4 v = *reinterpret_cast<const f32x4*>(ok ? xt + a_base[j] : p.x);
+                if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
+                R.a[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+#else
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-                if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+                if (ok) {
                     v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
                     if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
+#endif
             }
         } else {
             const int k = k0 + c8 * 4;
@@ -1100,9 +1115,24 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         mfmas(F0);
         read_frags(F1, buf, 1);
 #else
+#if X6B_IGLP
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         mfmas(F0);
         read_frags(F1, buf, 1);
         if (!late && !mid) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+#if X6B_IGLP
+        // Spread the split VALU, the LDS writes of stage k+1 and the fragment reads of the second
+        // half over the gaps of the second half's 24 MFMAs (an MFMA gap hides about 24 cycles of
+        // vector issue) instead of letting them bunch up after the last MFMA.
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x002, X6B_IGLP, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+        }
+#endif
 #endif
         __syncthreads();
     }
