@@ -139,6 +139,7 @@ CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads
     16: ("pw_splitk_kernel", 32, 32, 512), 17: ("pw_splitk_kernel", 32, 64, 512),
     21: ("conv_x6_kernel", 64, 64, 256), 22: ("conv_x6_kernel", 128, 64, 256), 23: ("conv_x6_kernel", 128, 128, 256), 24: ("conv_x6_kernel", 256, 128, 512),
     25: ("conv_x6b_kernel", 256, 128, 512), 27: ("conv_x6_kernel", 128, 64, 512), 28: ("conv_x6_kernel", 128, 128, 512),
+    29: ("conv_x6b_kernel", 128, 128, 512), 30: ("conv_x6b_kernel", 128, 128, 512),
 }
 
 

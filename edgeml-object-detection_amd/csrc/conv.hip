@@ -762,12 +762,16 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // PS: the input arrives pre-split (p.x3: three dense bf16 planes written by split_act_kernel, input
 // transform already applied), so a stage is 2 rows x 3 planes of 16-B loads per thread, stored to
 // LDS unchanged (requires UT, !XF).
-template <bool XF, bool UT, bool PS>
+// BM = 256: 4 x 2 waves of 64 x 64; BM = 128: 2 x 4 waves of 64 x 32 (twice the workgroups for the
+// small-M layers, half the MFMAs per barrier).  PF = 2: two register stages (loads two stages ahead,
+// B register-staged too) instead of the skewed one-register-stage pipeline.
+template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF>
 __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
-    constexpr bool GL = X6B_GLDS && X6B_PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
-    constexpr int WM = 4, WN = 2, TM = 2, TN = 2, NT = 512;
-    constexpr int BM = 256, BN = 128;
+    static_assert(BM == 256 || (BM == 128 && !PS), "x6b tiles: 256 x 128, or 128 x 128 without pre-split input");
+    constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
+    constexpr int WM = BM / 64, WN = 8 / WM, TM = 2, TN = 128 / (WN * 32), NT = 512;
+    constexpr int BN = 128;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
     constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
     constexpr int PA = BM * BK6B, PB = BN * BK6B;  // bf16 elements per plane
@@ -1053,7 +1057,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
             mfmas(F);
         }
     };
-#if X6B_PIPE
+    if constexpr (PF != 2 && X6B_PIPE) {
     // Skewed pipeline: the second K half of stage k-1 (fragments held in registers across the
     // barrier) runs while stage k's first-half fragments are read, and stage k+1's operands are
     // written to the other buffer under stage k's MFMAs, so the matrix pipe does not idle through
@@ -1126,7 +1130,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         // half over the gaps of the second half's 24 MFMAs (an MFMA gap hides about 24 cycles of
         // vector issue) instead of letting them bunch up after the last MFMA.
 #pragma unroll
-        for (int i = 0; i < 24; ++i) {
+        for (int i = 0; i < TM * TN * 6; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
             __builtin_amdgcn_sched_group_barrier(0x002, X6B_IGLP, 0);  // VALU
@@ -1137,7 +1141,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         __syncthreads();
     }
     mfmas(F1);
-#elif X6B_PF == 2
+    } else if constexpr (PF == 2) {
     // Two register stages: stage k+2's global loads are issued before stage k's MFMAs, stage k+1's
     // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
     // time to land.
@@ -1156,7 +1160,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         step(kc, r1, r0);
         if (kc + 1 < nk) step(kc + 1, r0, r1);
     }
-#else
+    } else {
     Regs r0;
     load_stage(r0, next_k(ca), 0);
     store_stage(r0, 0);
@@ -1168,7 +1172,7 @@ __global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
         if (kc + 1 < nk) store_stage(r0, buf ^ 1);
         __syncthreads();
     }
-#endif
+    }
 
     conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
 }
@@ -1218,6 +1222,7 @@ static int x6b_korder() {
     return v;
 }
 
+template <int BM = 256, int PF = X6B_PF>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     ConvParams p = p0;
     p.korder = x6b_korder();
@@ -1226,10 +1231,10 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     if (p.ksplit > 1)
         EDGEDET_REQUIRE(p.ksplit == 2 && !p.res && p.act == 0 && p.Kpad >= 2 * BK6B,
                         "conv split-K: 2 halves, no residual, no activation (y must be zeroed)");
-    const int64_t nwg = cdiv(p.M, 256) * cdiv(p.Cout, 128) * (p.ksplit > 1 ? 2 : 1);
+    const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, 128) * (p.ksplit > 1 ? 2 : 1);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
     const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
-    if (x6b_presplit(p)) {
+    if (BM == 256 && x6b_presplit(p)) {
         const int64_t items = (int64_t)p.B * p.H * p.W * (p.Cin / 8);
         const unsigned g = (unsigned)std::min<int64_t>(cdiv(items, 256), 256 * 64);
         hipLaunchKernelGGL(xf ? split_act_kernel<true> : split_act_kernel<false>, dim3(g), dim3(256), 0, s, p);
@@ -1238,8 +1243,8 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
         EDGEDET_LAUNCH_CHECK();
         return 0;
     }
-    auto k = xf ? (ut ? conv_x6b_kernel<true, true, false> : conv_x6b_kernel<true, false, false>)
-                : (ut ? conv_x6b_kernel<false, true, false> : conv_x6b_kernel<false, false, false>);
+    auto k = xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF> : conv_x6b_kernel<true, false, false, BM, PF>)
+                : (ut ? conv_x6b_kernel<false, true, false, BM, PF> : conv_x6b_kernel<false, false, false, BM, PF>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
@@ -1383,6 +1388,8 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 25: return launch_x6b(p, s);             // 256 x 128, bf16x6, 32-deep swizzled stages
         case 27: return launch_x6<4, 2, 1, 1>(p, s);  // 128 x 64, bf16x6, 8 waves (32 x 32 each)
         case 28: return launch_x6<4, 2, 1, 2>(p, s);  // 128 x 128, bf16x6, 8 waves (32 x 64 each)
+        case 29: return launch_x6b<128, 1>(p, s);     // 128 x 128, bf16x6, 32-deep swizzled stages, skewed pipeline
+        case 30: return launch_x6b<128, 2>(p, s);     // the same, two register stages
         case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
             ConvParams q = p;
             q.ksplit = 2;
