@@ -53,6 +53,7 @@
 //   RETINA_CLASS_NMS p0..4 level records (box,score,tb,label,count); p5..9 class records [B,K,kmax];
 //                  i0..4 B,L,kin,K,kmax; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
+#include <cstdlib>
 #include <mutex>
 #include <string>
 
@@ -124,8 +125,27 @@ static ConvParams conv_params(const edgedet_op& o) {
     return p;
 }
 
+// Diagnostic only (wrong results): EDGEDET_DIAG_SKIP=k1,k2,... launches nothing for ops of those
+// kinds, to measure what each op family costs the steady-state step under stream concurrency.
+static uint64_t diag_skip_mask() {
+    static const uint64_t m = [] {
+        uint64_t r = 0;
+        if (const char* e = std::getenv("EDGEDET_DIAG_SKIP"))
+            for (const char* q = e; *q;) {
+                char* end;
+                const long k = std::strtol(q, &end, 10);
+                if (end == q) break;
+                if (k > 0 && k < 64) r |= 1ull << k;
+                q = *end ? end + 1 : end;
+            }
+        return r;
+    }();
+    return m;
+}
+
 static int run_op(const edgedet_op& o, hipStream_t s) {
     const int64_t* I = o.i;
+    if ((diag_skip_mask() >> (o.kind & 63)) & 1 && o.kind != EDGEDET_OP_FORK && o.kind != EDGEDET_OP_JOIN) return 0;
     switch (o.kind) {
         case EDGEDET_OP_MEMSET:
             EDGEDET_CHECK_HIP(hipMemsetAsync(P<void>(o, 0), 0, (size_t)I[0], s));

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("d")
     ap.add_argument("--top", type=int, default=20)
+    ap.add_argument("--raw", action="store_true", help="every counter per wave (cycle counters as a share of SQ_WAVE_CYCLES)")
     a = ap.parse_args()
     f = glob.glob(os.path.join(a.d, "**", "*counter_collection.csv"), recursive=True)[0]
     disp = {}
@@ -35,6 +36,14 @@ def main():
             if c != "name":
                 g[c] = g.get(c, 0.0) + v
     rows = sorted(agg.items(), key=lambda kv: -kv[1]["ns"])[: a.top]
+    if a.raw:
+        for k, g in rows:
+            w = max(g.get("SQ_WAVES", 0.0), 1.0)
+            cyc = max(g.get("SQ_WAVE_CYCLES", 0.0), 1.0)
+            parts = [f"{c}={g[c] / cyc:.3f}" if c.startswith(("SQ_WAIT", "SQ_ACTIVE", "SQ_BUSY")) else f"{c}/w={g[c] / w:.1f}"
+                     for c in sorted(g) if c.startswith(("SQ_", "GRBM_", "TCC_", "TCP_")) and c != "SQ_WAVES"]
+            print(f"{k}: {g['n']} disp, {g['ns'] / g['n'] / 1e3:.1f} us, {w / g['n']:.0f} waves; " + ", ".join(parts))
+        return
     print(f"{'us/disp':>8} {'x':>4} {'waves':>7} {'valu/w':>7} {'lds/w':>6} {'salu/w':>6} {'cyc/w':>8} "
           f"{'ldswait':>7} {'conf/lds':>8}  kernel")
     for k, g in rows:
