@@ -409,7 +409,7 @@ def cpu_baseline(kind, budget_s=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=750)  # about 1 s of timed SSD work
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="both", choices=["ssd", "frcnn", "retinanet", "both", "all"])
     ap.add_argument("--retina-batch", type=int, default=8)

@@ -126,22 +126,27 @@ static ConvParams conv_params(const edgedet_op& o) {
 }
 
 // Diagnostic only (wrong results): EDGEDET_DIAG_SKIP=k1,k2,... launches nothing for ops of those
-// kinds, to measure what each op family costs the steady-state step under stream concurrency.
-static uint64_t diag_skip_mask() {
-    static const uint64_t m = [] {
-        uint64_t r = 0;
+// kinds (100 + t: convs whose requested tile is t), to measure what each op family costs the
+// steady-state step under stream concurrency.
+static const uint64_t* diag_skip_masks() {
+    static const uint64_t m[2] = {0, 0};
+    static const bool once = [] {
+        uint64_t* w = const_cast<uint64_t*>(m);
         if (const char* e = std::getenv("EDGEDET_DIAG_SKIP"))
             for (const char* q = e; *q;) {
                 char* end;
                 const long k = std::strtol(q, &end, 10);
                 if (end == q) break;
-                if (k > 0 && k < 64) r |= 1ull << k;
+                if (k > 0 && k < 64) w[0] |= 1ull << k;
+                if (k >= 100 && k < 164) w[1] |= 1ull << (k - 100);
                 q = *end ? end + 1 : end;
             }
-        return r;
+        return true;
     }();
+    (void)once;
     return m;
 }
+static uint64_t diag_skip_mask() { return diag_skip_masks()[0]; }
 
 static int run_op(const edgedet_op& o, hipStream_t s) {
     const int64_t* I = o.i;
@@ -196,6 +201,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             return mbconv_launch(p, s);
         }
         case EDGEDET_OP_CONV: {
+            if ((diag_skip_masks()[1] >> (I[23] & 63)) & 1) return 0;
             const ConvParams p = conv_params(o);
             EDGEDET_REQUIRE(p.K == p.KH * p.KW * p.Cin, "conv: K != KH*KW*Cin");
             return conv_launch(p, (int)I[23], s);
