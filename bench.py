@@ -43,8 +43,10 @@ def dist_setup(n_gpus):
     if world > 1:
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one rank per GPU over RCCL; EDGEDET_DIST_BACKEND=gloo with more ranks than GPUs rehearses
+        # the multi-rank logic on a one-GPU box (ranks share the device)
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dist.init_process_group(os.environ.get("EDGEDET_DIST_BACKEND", "nccl"))
         return dist, dist.get_rank(), world
     torch.cuda.set_device(0)
     return None, 0, 1
@@ -87,7 +89,7 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     el = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
@@ -140,6 +142,7 @@ CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads
     21: ("conv_x6_kernel", 64, 64, 256), 22: ("conv_x6_kernel", 128, 64, 256), 23: ("conv_x6_kernel", 128, 128, 256), 24: ("conv_x6_kernel", 256, 128, 512),
     25: ("conv_x6b_kernel", 256, 128, 512), 27: ("conv_x6_kernel", 128, 64, 512), 28: ("conv_x6_kernel", 128, 128, 512),
     29: ("conv_x6b_kernel", 128, 128, 512), 30: ("conv_x6b_kernel", 128, 128, 512),
+    31: ("conv_x6b_kernel", 64, 128, 512), 32: ("conv_x6b_kernel", 64, 128, 512),
 }
 
 

@@ -763,14 +763,15 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // transform already applied), so a stage is 2 rows x 3 planes of 16-B loads per thread, stored to
 // LDS unchanged (requires UT, !XF).
 // BM = 256: 4 x 2 waves of 64 x 64; BM = 128: 2 x 4 waves of 64 x 32 (twice the workgroups for the
-// small-M layers, half the MFMAs per barrier).  PF = 2: two register stages (loads two stages ahead,
-// B register-staged too) instead of the skewed one-register-stage pipeline.
+// small-M layers, half the MFMAs per barrier); BM = 64: 2 x 4 waves of 32 x 32, 72 KiB of LDS and at
+// most 128 VGPRs, so two workgroups (four waves per SIMD) share a CU.  PF = 2: two register stages
+// (loads two stages ahead, B register-staged too) instead of the skewed one-register-stage pipeline.
 template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF>
-__global__ void __launch_bounds__(512) conv_x6b_kernel(ConvParams p) {
+__global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
-    static_assert(BM == 256 || (BM == 128 && !PS), "x6b tiles: 256 x 128, or 128 x 128 without pre-split input");
+    static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
     constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
-    constexpr int WM = BM / 64, WN = 8 / WM, TM = 2, TN = 128 / (WN * 32), NT = 512;
+    constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM, TM = BM / (WM * 32), TN = 128 / (WN * 32), NT = 512;
     constexpr int BN = 128;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
     constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
@@ -1390,6 +1391,8 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 28: return launch_x6<4, 2, 1, 2>(p, s);  // 128 x 128, bf16x6, 8 waves (32 x 64 each)
         case 29: return launch_x6b<128, 1>(p, s);     // 128 x 128, bf16x6, 32-deep swizzled stages, skewed pipeline
         case 30: return launch_x6b<128, 2>(p, s);     // the same, two register stages
+        case 31: return launch_x6b<64, 1>(p, s);      // 64 x 128, bf16x6, two workgroups per CU
+        case 32: return launch_x6b<64, 2>(p, s);      // the same, two register stages
         case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
             ConvParams q = p;
             q.ksplit = 2;

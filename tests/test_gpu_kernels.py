@@ -272,7 +272,7 @@ def test_split_bf16x3_device_matches_host():
     assert np.array_equal(got, split_bf16x3(w.numpy()))
 
 
-@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25, 27, 28, 29, 30])
+@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25, 27, 28, 29, 30, 31, 32])
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 7, 8)])
 def test_conv_bf16x6_matches_torch(case, tile):
     _conv_case(*case, tile=tile, x6=True)
@@ -325,7 +325,7 @@ def test_conv_bf16x6_split_k(case):
     assert torch.equal(y1, y2)
 
 
-@pytest.mark.parametrize("tile", [22, 23, 24, 25, 29, 30])
+@pytest.mark.parametrize("tile", [22, 23, 24, 25, 29, 30, 31, 32])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)
 
