@@ -766,10 +766,13 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // small-M layers, half the MFMAs per barrier); BM = 64: 2 x 4 waves of 32 x 32, 72 KiB of LDS and at
 // most 128 VGPRs, so two workgroups (four waves per SIMD) share a CU.  PF = 2: two register stages
 // (loads two stages ahead, B register-staged too) instead of the skewed one-register-stage pipeline.
-template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF>
+// P1: 1x1, stride 1, dense input (p.lin_x, Cin % 32 == 0): a stage's k0 is the channel, and rows
+// past M load row 0 (their outputs are never stored), so the A loads need no tap or bounds work.
+template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF, bool P1 = false>
 __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
+    static_assert(!P1 || (UT && !PS), "pointwise stages: uniform taps, fp32 input");
     constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
     constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM, TM = BM / (WM * 32), TN = 128 / (WN * 32), NT = 512;
     constexpr int BN = 128;
@@ -898,6 +901,15 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
                             ok ? *reinterpret_cast<const uint4*>(xt + pl * x3plane + a_base[j]) : uint4{0u, 0u, 0u, 0u};
                 }
             }
+        } else if constexpr (P1) {
+            const int ci = k0 + c8 * 4;
+            const float* xt = p.x + ci;
+#pragma unroll
+            for (int j = 0; j < AJ; ++j) {
+                f32x4 v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
+                if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
+                R.a[j] = v;
+            }
         } else if constexpr (UT) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
             const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
@@ -994,7 +1006,7 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
     // instead (the KH*KW taps of one 32-channel chunk back to back, k = tap * Cin + 32 * chunk), so
     // the chunk's input window is re-read from L2 across the taps rather than from HBM.  Stages are
     // loaded strictly in order, so the position advances by one per load.
-    const bool cm = UT && p.korder && KHW > 1 && p.Kpad == KHW * p.Cin;
+    const bool cm = !P1 && UT && p.korder && KHW > 1 && p.Kpad == KHW * p.Cin;
     struct Cursor {
         int tap, chunk, k;
     };
@@ -1223,6 +1235,15 @@ static int x6b_korder() {
     return v;
 }
 
+// The pointwise specialisation of conv_x6b_kernel (EDGEDET_X6B_P1=0: the general uniform-tap form).
+static bool x6b_p1() {
+    static const bool v = [] {
+        const char* e = std::getenv("EDGEDET_X6B_P1");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 template <int BM = 256, int PF = X6B_PF>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     ConvParams p = p0;
@@ -1244,8 +1265,10 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
         EDGEDET_LAUNCH_CHECK();
         return 0;
     }
-    auto k = xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF> : conv_x6b_kernel<true, false, false, BM, PF>)
-                : (ut ? conv_x6b_kernel<false, true, false, BM, PF> : conv_x6b_kernel<false, false, false, BM, PF>);
+    const bool p1 = ut && p.lin_x && p.KH == 1 && p.KW == 1 && x6b_p1();
+    auto k = p1 ? (xf ? conv_x6b_kernel<true, true, false, BM, PF, true> : conv_x6b_kernel<false, true, false, BM, PF, true>)
+         : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF> : conv_x6b_kernel<true, false, false, BM, PF>)
+              : (ut ? conv_x6b_kernel<false, true, false, BM, PF> : conv_x6b_kernel<false, false, false, BM, PF>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
