@@ -766,13 +766,14 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // small-M layers, half the MFMAs per barrier); BM = 64: 2 x 4 waves of 32 x 32, 72 KiB of LDS and at
 // most 128 VGPRs, so two workgroups (four waves per SIMD) share a CU.  PF = 2: two register stages
 // (loads two stages ahead, B register-staged too) instead of the skewed one-register-stage pipeline.
-// P1: 1x1, stride 1, dense input (p.lin_x, Cin % 32 == 0): a stage's k0 is the channel, and rows
-// past M load row 0 (their outputs are never stored), so the A loads need no tap or bounds work.
+// P1: 1x1, stride 1, dense input (p.lin_x): a stage's k0 is the channel, and rows past M load row 0
+// (their outputs are never stored), so the A loads need no tap or bounds work; with Cin % 32 != 0
+// (!UT) the chunks past Cin are zeroed (they meet the zero weight padding).
 template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF, bool P1 = false>
 __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
-    static_assert(!P1 || (UT && !PS), "pointwise stages: uniform taps, fp32 input");
+    static_assert(!P1 || !PS, "pointwise stages: fp32 input");
     constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
     constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM, TM = BM / (WM * 32), TN = 128 / (WN * 32), NT = 512;
     constexpr int BN = 128;
@@ -906,8 +907,11 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
             const float* xt = p.x + ci;
 #pragma unroll
             for (int j = 0; j < AJ; ++j) {
-                f32x4 v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
-                if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
+                // (a chunk past Cin loads from p.x: past the last pixel it would leave the buffer)
+                const bool cok = UT || ci < p.Cin;
+                f32x4 v = *reinterpret_cast<const f32x4*>(cok ? xt + a_base[j] : p.x);
+                if constexpr (XF) v = in_transform(p, v, a_b[j], cok ? ci : 0);
+                if constexpr (!UT) v = cok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
                 R.a[j] = v;
             }
         } else if constexpr (UT) {
@@ -1265,8 +1269,9 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
         EDGEDET_LAUNCH_CHECK();
         return 0;
     }
-    const bool p1 = ut && p.lin_x && p.KH == 1 && p.KW == 1 && x6b_p1();
-    auto k = p1 ? (xf ? conv_x6b_kernel<true, true, false, BM, PF, true> : conv_x6b_kernel<false, true, false, BM, PF, true>)
+    const bool p1 = p.lin_x && p.KH == 1 && p.KW == 1 && p.Cin % 4 == 0 && x6b_p1();
+    auto k = p1 ? (xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, true> : conv_x6b_kernel<true, false, false, BM, PF, true>)
+                      : (ut ? conv_x6b_kernel<false, true, false, BM, PF, true> : conv_x6b_kernel<false, false, false, BM, PF, true>))
          : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF> : conv_x6b_kernel<true, false, false, BM, PF>)
               : (ut ? conv_x6b_kernel<false, true, false, BM, PF> : conv_x6b_kernel<false, false, false, BM, PF>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);

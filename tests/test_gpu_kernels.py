@@ -325,6 +325,17 @@ def test_conv_bf16x6_split_k(case):
     assert torch.equal(y1, y2)
 
 
+@pytest.mark.parametrize("tile", [25, 29, 30, 31, 32])
+@pytest.mark.parametrize("se", [False, True])
+@pytest.mark.parametrize("case", [(2, 9, 9, 16, 16, 1, 1, None, True), (3, 11, 7, 24, 72, 1, 1, "HS", False),
+                                  (2, 13, 10, 40, 120, 1, 1, "RE", False), (1, 20, 20, 72, 24, 1, 1, None, True)])
+def test_conv_bf16x6_pointwise_ragged_cin(case, se, tile):
+    """The pointwise x6b form with Cin not a multiple of 32: the chunks past Cin are zeroed (and load
+    from a safe address: past the last pixel they would leave the buffer), with and without the SE
+    input scale."""
+    _conv_case(*case, tile=tile, se=se, x6=True)
+
+
 @pytest.mark.parametrize("tile", [22, 23, 24, 25, 29, 30, 31, 32])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)
