@@ -855,7 +855,18 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
     // x3 scratch: X3Z zero elements (the source of padding taps under LDS-DMA), then the three planes
     const unsigned short* x3 = reinterpret_cast<const unsigned short*>(p.x3);
     // la / lb: load the stage's A rows (to registers, or to LDS by DMA under PS && GL) / its B rows
-    auto load_part = [&](Regs& R, int k0, int bbuf, bool la, bool lb) {
+    // A stage's K position: k0, and (uniform-tap stages, channel-chunk-major order) its filter tap
+    // and first channel, advanced incrementally by the cursor below
+    struct StageK {
+        int k0, kh, kw, ci;
+    };
+    auto stage_tap = [&](const StageK& sk, int& kh, int& kw, int& ci0) {
+        kh = sk.kh;
+        kw = sk.kw;
+        ci0 = sk.ci;
+    };
+    auto load_part = [&](Regs& R, const StageK& sk, int bbuf, bool la, bool lb) {
+        const int k0 = sk.k0;
         if (GL && lb) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
             // -> the 16-B slot l of the block); the swizzle is applied on the source address
@@ -870,11 +881,10 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
         }
         if (!la) {
         } else if constexpr (PS) {
-            const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
-            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
-            const int kw = tap - kh * p.KW;
+            int kh, kw, ci0;
+            stage_tap(sk, kh, kw, ci0);
             if constexpr (GL) {
-                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin);
+                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + ci0;
 #pragma unroll
                 for (int j = 0; j < AJ; ++j) {
                     const int row = a_row0 + AST * j;
@@ -891,7 +901,7 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
                             16, 0, 0);
                 }
             } else {
-                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + (k0 - tap * p.Cin) + 8 * (tid & 3);
+                const unsigned short* xt = x3 + X3Z + (int64_t)(kh * p.W + kw) * p.Cin + ci0 + 8 * (tid & 3);
 #pragma unroll
                 for (int j = 0; j < AJ; ++j) {
                     const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
@@ -915,10 +925,9 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
                 R.a[j] = v;
             }
         } else if constexpr (UT) {
-            const int tap = (int)fdiv((uint32_t)k0, p.div_cin);  // uniform
-            const int kh = (int)fdiv((uint32_t)tap, p.div_kw);
-            const int kw = tap - kh * p.KW;
-            const int ci = k0 - tap * p.Cin + c8 * 4;
+            int kh, kw, ci0;
+            stage_tap(sk, kh, kw, ci0);
+            const int ci = ci0 + c8 * 4;
             const float* xt = p.x + (int64_t)(kh * p.W + kw) * p.x_pstride + ci;
 #pragma unroll
             for (int j = 0; j < AJ; ++j) {
@@ -963,7 +972,7 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
                 R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
         }
     };
-    auto load_stage = [&](Regs& R, int k0, int bbuf) { load_part(R, k0, bbuf, true, true); };
+    auto load_stage = [&](Regs& R, const StageK& sk, int bbuf) { load_part(R, sk, bbuf, true, true); };
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
@@ -1006,28 +1015,39 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
     const int kbeg = ksp > 1 ? (blockIdx.x & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
     const int nk = ksp > 1 ? ((blockIdx.x & 1) ? nk_all - kbeg : (nk_all + 1) / 2) : nk_all;
     // Stage order. Tap-major (stage s at k = 32 s, the weight layout) sweeps a block's whole input
-    // panel once per filter tap; with p.korder and a uniform tap the stages run channel-chunk-major
-    // instead (the KH*KW taps of one 32-channel chunk back to back, k = tap * Cin + 32 * chunk), so
-    // the chunk's input window is re-read from L2 across the taps rather than from HBM.  Stages are
-    // loaded strictly in order, so the position advances by one per load.
-    const bool cm = !P1 && UT && p.korder && KHW > 1 && p.Kpad == KHW * p.Cin;
+    // panel once per filter tap; with a uniform tap the stages run channel-chunk-major instead (the
+    // KH*KW taps of one 32-channel chunk back to back, k = tap * Cin + 32 * chunk; K = KH*KW*Cin is
+    // then Kpad), so the chunk's input window is re-read from L2 across the taps rather than from
+    // HBM.  Stages are loaded strictly in order, so the cursor advances by one per load, tap and
+    // channel incrementally (no divisions in the loop).
+    constexpr bool cm = UT && !P1;
     struct Cursor {
-        int tap, chunk, k;
+        int tap, chunk, k, kh, kw;
     };
-    Cursor ca{cm ? kbeg % KHW : 0, cm ? kbeg / KHW : 0, kbeg * BK6B};
+    Cursor ca{cm ? kbeg % KHW : 0, cm ? kbeg / KHW : 0, kbeg * BK6B, 0, 0};
+    if constexpr (cm) {
+        ca.kh = ca.tap / p.KW;
+        ca.kw = ca.tap - ca.kh * p.KW;
+    }
     auto next_k = [&](Cursor& c) {
-        int k0;
-        if (cm) {
-            k0 = c.tap * p.Cin + c.chunk * BK6B;
-            if (++c.tap == KHW) {
+        StageK sk;
+        if constexpr (cm) {
+            sk = StageK{c.tap * p.Cin + c.chunk * BK6B, c.kh, c.kw, c.chunk * BK6B};
+            ++c.tap;
+            if (++c.kw == p.KW) {
+                c.kw = 0;
+                ++c.kh;
+            }
+            if (c.tap == KHW) {
                 c.tap = 0;
+                c.kh = 0;
                 ++c.chunk;
             }
         } else {
-            k0 = c.k;
+            sk = StageK{c.k, -1, 0, 0};
             c.k += BK6B;
         }
-        return k0;
+        return sk;
     };
     Cursor cb = ca;  // the B rows' cursor (runs behind ca in the late wave group of the stagger)
     const int h = lane >> 5;
@@ -1229,16 +1249,6 @@ static bool x6b_presplit(const ConvParams& p) {
     return p.x3 && p.Cin % BK6B == 0 && p.x_pstride % 4 == 0 && ((uintptr_t)p.x3 & 15) == 0;
 }
 
-// Channel-chunk-major K stages in conv_x6b_kernel (EDGEDET_X6B_KORDER=0: tap-major, the order of
-// the weight layout).  Changes the fp32 accumulation order, not the terms summed.
-static int x6b_korder() {
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_X6B_KORDER");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-
 // The pointwise specialisation of conv_x6b_kernel (EDGEDET_X6B_P1=0: the general uniform-tap form).
 static bool x6b_p1() {
     static const bool v = [] {
@@ -1250,8 +1260,7 @@ static bool x6b_p1() {
 
 template <int BM = 256, int PF = X6B_PF>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
-    ConvParams p = p0;
-    p.korder = x6b_korder();
+    const ConvParams& p = p0;
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
     EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
     if (p.ksplit > 1)
