@@ -197,7 +197,7 @@ class _Detector:
         contract's float [3,H,W] tensors or the decoded uint8 [3,H,W] images (detect.py:57), which
         cross PCIe as bytes (4x fewer than float) and are divided by 255 on the device, bit-identical
         to the host's `image / 255` (detect.py:58).  Same arithmetic as __call__ (same plan
-        lowering, same kernels)."""
+        lowering, same kernels, replayed from a hipGraph per slot)."""
         if self.device is None:
             self.to("cuda")
         n = max(1, int(inflight or self.INFLIGHT))
@@ -271,9 +271,13 @@ class _Detector:
                 for j, im in enumerate(whole if whole is not None else imgs):
                     stage[j].copy_(im if key[3] else im.to(torch.float32))
                 src = stage
+            if plan.graph is None:
+                # one hipGraph per slot plan (captured on first use): a batch is then one launch
+                # instead of a host call per op, which kept the host, not the device, the bottleneck
+                plan.capture(stream)
             with torch.cuda.stream(stream):
                 plan.input.tensor().copy_(src, non_blocking=True)
-                plan.run(stream)
+                plan.replay(stream)
                 sl["count"].copy_(plan.out_count.tensor(), non_blocking=True)
                 sl["box"].copy_(plan.out_box.tensor(), non_blocking=True)
                 sl["score"].copy_(plan.out_score.tensor(), non_blocking=True)
@@ -292,6 +296,9 @@ class SSDLite320(_Detector):
 
     kind = "ssd"
     BN_EPS = 1e-3
+    # run_batches slots: four batches in flight hide the per-batch host work (upload issue, D2H wait,
+    # row formatting) behind the device (end to end 18.3k -> 25.2k img/s, tools/e2e_sweep.py)
+    INFLIGHT = 4
     SIZE = 320
     SCORE_THRESH, NMS_THRESH, DETS, TOPK = 0.001, 0.55, 300, 300
     max_batch = 64
