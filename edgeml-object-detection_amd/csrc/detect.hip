@@ -684,14 +684,35 @@ __device__ __forceinline__ int wave_select_topk(const float* __restrict__ sc, in
     uint32_t T = 1u;
     int need_eq = 0;
     if (!take_all) {
-        uint64_t lo = 1, hi = 1ull << 32;
+        // bisection on [min key, max key + 1): count(>= lo) >= topk > count(>= hi), then T = lo, the
+        // topk-th largest key.  (Interpolating the probes between the two counts measured slower:
+        // 52 against 42 us per 16-image chain.)
+        uint32_t kmn = 0xffffffffu, kmx = 0u;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            kmn = kr[j] != 0u && kr[j] < kmn ? kr[j] : kmn;
+            kmx = kr[j] > kmx ? kr[j] : kmx;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t a = (uint32_t)__shfl_xor((int)kmn, o), b = (uint32_t)__shfl_xor((int)kmx, o);
+            kmn = a < kmn ? a : kmn;
+            kmx = b > kmx ? b : kmx;
+        }
+        uint64_t lo = kmn, hi = (uint64_t)kmx + 1;
+        int chi = 0;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
-            if (count_ge((uint32_t)mid) >= topk) lo = mid;
-            else hi = mid;
+            const int c = count_ge((uint32_t)mid);
+            if (c >= topk) {
+                lo = mid;
+            } else {
+                hi = mid;
+                chi = c;
+            }
         }
         T = (uint32_t)lo;
-        need_eq = topk - ((hi >> 32) ? 0 : count_ge((uint32_t)hi));
+        need_eq = topk - chi;
     }
     int written = 0, eq_taken = 0;
 #pragma unroll
