@@ -129,9 +129,9 @@ static ConvParams conv_params(const edgedet_op& o) {
 // kinds (100 + t: convs whose requested tile is t), to measure what each op family costs the
 // steady-state step under stream concurrency.
 static const uint64_t* diag_skip_masks() {
-    static const uint64_t m[2] = {0, 0};
+    static uint64_t m[2] = {0, 0};
     static const bool once = [] {
-        uint64_t* w = const_cast<uint64_t*>(m);
+        uint64_t* w = m;
         if (const char* e = std::getenv("EDGEDET_DIAG_SKIP"))
             for (const char* q = e; *q;) {
                 char* end;
