@@ -473,6 +473,116 @@ __global__ void __launch_bounds__(NW * 64) pw_splitk_kernel(ConvParams p) {
     conv_epilogue<1, TN>(p, acc, m0, n0, h, l32);
 }
 
+// Streaming pointwise conv for the narrow HBM-bound 1x1 layers of the SSDLite early blocks (Cin <=
+// 72, Cout <= 96, 16-image chains at 160^2 / 80^2 / 40^2): each wave walks 32-row blocks of the
+// output with a grid stride, the next block's A rows in flight while the current one is multiplied
+// and stored, so a wave never idles on one load-compute-store chain the way the one-tile-per-wave
+// kernels do.  Exact fp32 MFMA (32x32x2): lane (r, h) holds A[row r][k = 8j + 4h + e] and the
+// weight B[k][col r] for the same k (any consistent K order is a valid summation order), so K runs
+// in 8-deep chunks (KJ = ceil(Cin / 8)) instead of the 32-deep padding, and the whole weight matrix
+// (NB column blocks of 32 x KJ chunks) stays in registers for the wave's lifetime.
+// ncg > 1: the Cout columns are split over ncg wave groups of NB blocks each (wave w takes column
+// group w % ncg), so a wave's weights and accumulators stay small; PF: prefetch the next block.
+template <int NB, int KJ, bool XF, bool PF>
+__global__ void __launch_bounds__(256) pw_stream_kernel(ConvParams p, int ncg) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int nblk = (p.M + 31) / 32;
+    const int wg = blockIdx.x * 4 + (threadIdx.x >> 6), nwg = gridDim.x * 4;
+    const int cg = wg % ncg, gw = wg / ncg, nw = nwg / ncg;
+    if (gw >= nblk || gw >= nw) return;
+    const int n0 = cg * 32 * NB;
+    f32x4 wb[NB][KJ];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + 32 * nb + r;
+        const float* wr = p.w + (int64_t)(n < p.Cout ? n : 0) * p.Kpad + 4 * h;
+#pragma unroll
+        for (int j = 0; j < KJ; ++j)
+            wb[nb][j] = n < p.Cout ? *reinterpret_cast<const f32x4*>(wr + 8 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto load_a = [&](int blk, f32x4 (&v)[KJ]) {
+        const int m = blk * 32 + r;
+        const bool ok = m < p.M;
+        const float* row = p.x + (int64_t)(ok ? m : 0) * p.x_pstride + 4 * h;
+        const int b = XF && ok ? (int)fdiv((uint32_t)m, p.div_howo) : 0;
+#pragma unroll
+        for (int j = 0; j < KJ; ++j) {
+            const int k = 8 * j + 4 * h;
+            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (ok && k < p.Cin) {
+                x = *reinterpret_cast<const f32x4*>(row + 8 * j);
+                if constexpr (XF) x = in_transform(p, x, b, k);
+            }
+            v[j] = x;
+        }
+    };
+    f32x4 a[KJ];
+    if (PF) load_a(gw, a);
+    for (int blk = gw; blk < nblk; blk += nw) {
+        const bool more = PF && blk + nw < nblk;
+        f32x4 an[KJ];
+        if (more) load_a(blk + nw, an);
+        if (!PF) load_a(blk, a);
+        floatx16 acc[1][NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[0][nb][q] = 0.f;
+#pragma unroll
+        for (int j = 0; j < KJ; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+                    acc[0][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j][e], wb[nb][j][e], acc[0][nb], 0, 0, 0);
+        // lean epilogue (dense y and residual rows, checked by the launcher): one base address per
+        // lane, row offsets (r & 3) + 8 (r >> 2) times the uniform pixel stride
+        const int mb = blk * 32 + 4 * h;
+        float bj[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) bj[nb] = p.bias[n0 + 32 * nb + r < p.Cout ? n0 + 32 * nb + r : 0];
+        if (p.res) {
+            const float* rb = p.res + (int64_t)mb * p.res_pstride + n0 + r;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int dm = (q & 3) + 8 * (q >> 2);
+                const bool ok = mb + dm < p.M;
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+                    const bool cok = ok && n0 + 32 * nb + r < p.Cout;
+                    acc[0][nb][q] = (acc[0][nb][q] + bj[nb]) + (cok ? rb[(int64_t)dm * p.res_pstride + 32 * nb] : 0.f);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[0][nb][q] += bj[nb];
+        }
+        switch (p.act) {
+            case ACT_RELU: act_tile<1, NB, ACT_RELU>(acc); break;
+            case ACT_RELU6: act_tile<1, NB, ACT_RELU6>(acc); break;
+            case ACT_HSWISH: act_tile<1, NB, ACT_HSWISH>(acc); break;
+            case ACT_HSIGMOID: act_tile<1, NB, ACT_HSIGMOID>(acc); break;
+            case ACT_SIGMOID: act_tile<1, NB, ACT_SIGMOID>(acc); break;
+            default: break;
+        }
+        float* yb = p.y + p.y_off + (int64_t)mb * p.y_pstride + n0 + r;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int dm = (q & 3) + 8 * (q >> 2);
+            if (mb + dm < p.M)
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+                    if (n0 + 32 * nb + r < p.Cout) yb[(int64_t)dm * p.y_pstride + 32 * nb] = acc[0][nb][q];
+        }
+        if (more)
+#pragma unroll
+            for (int j = 0; j < KJ; ++j) a[j] = an[j];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // fp32 GEMM through the bf16 matrix cores: the six-term split ("bf16x6").
 //
@@ -1449,6 +1559,52 @@ static int launch_pw_splitk(const ConvParams& p, hipStream_t s) {
     return 0;
 }
 
+// Tiles 33-35 (pw_stream_kernel): 1x1 dense input and output rows, Cin <= 72, Cout <= 96.
+// 33: every column block in one wave (weights of NB x KJ <= 18 chunks in registers); 34: one
+// column block per wave (column groups over the waves), next block prefetched; 35: 34 without the
+// prefetch (more waves per SIMD instead).
+template <int NB, int KJ, bool PF>
+static int launch_pw_stream_nk(const ConvParams& p, hipStream_t s) {
+    const int ncg = (p.Cout + 32 * NB - 1) / (32 * NB);
+    const int64_t waves = cdiv(p.M, 32) * ncg;
+    const unsigned g = (unsigned)std::min<int64_t>(cdiv(waves, 4), 256 * 8);
+    const bool xf = p.in_scale || p.in_shift || p.in_relu;
+    auto k = xf ? pw_stream_kernel<NB, KJ, true, PF> : pw_stream_kernel<NB, KJ, false, PF>;
+    hipLaunchKernelGGL(k, dim3(g), dim3(256), 0, s, p, ncg);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int NB, bool PF>
+static int launch_pw_stream_n(const ConvParams& p, int kj, hipStream_t s) {
+    switch (kj) {
+        case 1: case 2: return launch_pw_stream_nk<NB, 2, PF>(p, s);
+        case 3: return launch_pw_stream_nk<NB, 3, PF>(p, s);
+        case 4: return launch_pw_stream_nk<NB, 4, PF>(p, s);
+        case 5: return launch_pw_stream_nk<NB, 5, PF>(p, s);
+        case 6: return launch_pw_stream_nk<NB, 6, PF>(p, s);
+        case 7: case 8: if constexpr (NB <= 2) return launch_pw_stream_nk<NB, 8, PF>(p, s); break;
+        case 9: if constexpr (NB <= 2) return launch_pw_stream_nk<NB, 9, PF>(p, s); break;
+        default: break;
+    }
+    EDGEDET_REQUIRE(false, "pw_stream: Cin / Cout outside the register-resident weight shapes");
+    return -1;
+}
+
+static int launch_pw_stream(const ConvParams& p, int tile, hipStream_t s) {
+    EDGEDET_REQUIRE(p.lin_x && p.KH == 1 && p.KW == 1, "pw_stream needs a 1x1/stride-1 dense input");
+    EDGEDET_REQUIRE(p.ksplit <= 1, "pw_stream: no split-K");
+    EDGEDET_REQUIRE(p.lin_y && (!p.res || p.lin_res), "pw_stream: dense output and residual rows");
+    const int kj = (p.Cin + 7) / 8, nb = (p.Cout + 31) / 32;
+    EDGEDET_REQUIRE(nb >= 1 && nb <= 3 && kj <= 9, "pw_stream: Cout <= 96, Cin <= 72");
+    if (tile == 34) return launch_pw_stream_n<1, true>(p, kj, s);
+    if (tile == 35) return launch_pw_stream_n<1, false>(p, kj, s);
+    EDGEDET_REQUIRE(nb * kj <= 18, "pw_stream tile 33: NB x KJ <= 18");
+    if (nb == 1) return launch_pw_stream_n<1, true>(p, kj, s);
+    if (nb == 2) return launch_pw_stream_n<2, true>(p, kj, s);
+    return launch_pw_stream_n<3, true>(p, kj, s);
+}
+
 template <int WM, int WN, int TM, int TN>
 static int launch_cfg(const ConvParams& p, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -1548,6 +1704,9 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
             q.ksplit = 2;
             return launch_x6b(q, s);
         }
+        case 33:                                      // streaming 1x1, fp32 MFMA, weights in registers
+        case 34:
+        case 35: return launch_pw_stream(p, tile, s);
         case 1: return launch_cfg<4, 1, 1, 1>(p, s);  // 128 x 32
         case 2: return launch_cfg<2, 2, 2, 1>(p, s);  // 128 x 64
         case 3: return launch_cfg<2, 2, 2, 2>(p, s);  // 128 x 128

@@ -80,6 +80,28 @@ def test_conv_direct_pointwise(case, tile, se):
     _conv_case(*case, tile=tile, se=se)
 
 
+@pytest.mark.parametrize("tile", [33, 34, 35])
+@pytest.mark.parametrize("case", [(2, 33, 31, 24, 72, 1, 1, "RE", False), (1, 9, 9, 16, 16, 1, 1, None, True),
+                                  (2, 13, 11, 64, 24, 1, 1, "R6", False), (3, 20, 20, 72, 24, 1, 1, None, True),
+                                  (2, 17, 19, 16, 64, 1, 1, "HS", False), (2, 10, 10, 72, 40, 1, 1, None, False),
+                                  (1, 7, 7, 40, 96, 1, 1, "RE", True), (2, 40, 40, 20, 36, 1, 1, "HS", False)])
+@pytest.mark.parametrize("se", [False, True])
+def test_conv_pointwise_stream(case, tile, se):
+    """Tiles 33-35, the streaming 1x1 kernel of the narrow SSDLite layers (exact fp32 MFMA, 8-deep K
+    chunks, weights in registers): ragged row blocks, a Cin that is not a multiple of 8, residual,
+    SE input scale, Cout not a multiple of 32."""
+    _conv_case(*case, tile=tile, se=se)
+
+
+def test_conv_pointwise_stream_refuses_wide():
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight
+    x = torch.randn(1, 4, 4, 480, device=DEV)
+    wp = torch.from_numpy(pack_conv_weight(torch.randn(128, 480, 1, 1).numpy())[0]).to(DEV)
+    with pytest.raises(ops.EdgeDetError):
+        ops.conv2d_nhwc(x, wp, torch.zeros(128, device=DEV), 128, 1, 1, 0, None, tile=33)
+
+
 @pytest.mark.parametrize("B,H,W,C,k,s,act", [(2, 20, 20, 72, 5, 2, "RE"), (3, 10, 10, 672, 5, 1, "HS"),
                                               (2, 3, 3, 128, 3, 2, "R6"), (1, 40, 40, 64, 3, 1, "RE"),
                                               (2, 13, 7, 16, 3, 2, "RE"), (1, 1, 1, 480, 3, 2, "HS"),

@@ -22,6 +22,11 @@ SHAPES = {  # name: (B, H, W, Cin, Cout, k, stride)
     "ssd_12_3": (16, 20, 20, 672, 112, 1, 1),
     "retina_cls": (8, 100, 100, 256, 819, 3, 1),
     "ssd_head_cls1b": (16, 10, 10, 480, 546, 1, 1),
+    "ssd_02_expand": (16, 160, 160, 16, 64, 1, 1),
+    "ssd_02_project": (16, 80, 80, 64, 24, 1, 1),
+    "ssd_03_expand": (16, 80, 80, 24, 72, 1, 1),
+    "ssd_03_project": (16, 80, 80, 72, 24, 1, 1),
+    "ssd_04_project": (16, 40, 40, 72, 40, 1, 1),
 }
 
 
