@@ -1563,11 +1563,19 @@ static int launch_pw_splitk(const ConvParams& p, hipStream_t s) {
 // 33: every column block in one wave (weights of NB x KJ <= 18 chunks in registers); 34: one
 // column block per wave (column groups over the waves), next block prefetched; 35: 34 without the
 // prefetch (more waves per SIMD instead).
+static int pw_stream_max_wg() {  // grid cap (EDGEDET_PWS_WG: A/B of waves per block-walk)
+    static const int v = [] {
+        const char* e = std::getenv("EDGEDET_PWS_WG");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 256 * 8;
+    }();
+    return v;
+}
+
 template <int NB, int KJ, bool PF>
 static int launch_pw_stream_nk(const ConvParams& p, hipStream_t s) {
     const int ncg = (p.Cout + 32 * NB - 1) / (32 * NB);
     const int64_t waves = cdiv(p.M, 32) * ncg;
-    const unsigned g = (unsigned)std::min<int64_t>(cdiv(waves, 4), 256 * 8);
+    const unsigned g = (unsigned)std::min<int64_t>(cdiv(waves, 4), pw_stream_max_wg());
     const bool xf = p.in_scale || p.in_shift || p.in_relu;
     auto k = xf ? pw_stream_kernel<NB, KJ, true, PF> : pw_stream_kernel<NB, KJ, false, PF>;
     hipLaunchKernelGGL(k, dim3(g), dim3(256), 0, s, p, ncg);
