@@ -439,7 +439,8 @@ static void conv_op(Plan& P, const ConvArgs& a) {
         }
     }
     const bool xf = a.in_scale.kind != Ref::NONE || a.in_shift.kind != Ref::NONE || a.in_relu;
-    if (env_int("EDGEDET_CONV_PRESPLIT", 1) == 1 && xf && w3 && C % 32 == 0 && (o.i[23] == 0 || o.i[23] == 25))
+    const int presplit = env_int("EDGEDET_CONV_PRESPLIT", 1);
+    if (presplit != 0 && (xf || presplit == 2) && w3 && C % 32 == 0 && (o.i[23] == 0 || o.i[23] == 25))
         o.p[8] = P.ref(P.x3_scratch(3 * B * H * W * C + 32));
     P.add(o);
 }

@@ -33,7 +33,8 @@ if CONV_MATH not in ("bf16x6", "f32"):
 _TILES_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "conv_tiles_gfx950.json")
 # Pre-split conv inputs for the 256 x 128 bf16x6 tile (csrc/conv.hip split_act_kernel): one x3 scratch
 # per lane, sized for the largest input it serves.  EDGEDET_CONV_PRESPLIT=0 keeps the in-loop split.
-CONV_PRESPLIT = os.environ.get("EDGEDET_CONV_PRESPLIT", "1") == "1"
+# EDGEDET_CONV_PRESPLIT=2 pre-splits every eligible tile-25 input (A/B of the plain-input case).
+CONV_PRESPLIT = int(os.environ.get("EDGEDET_CONV_PRESPLIT", "1"))
 CONV_TILES = {}
 if os.path.exists(_TILES_PATH) and os.environ.get("EDGEDET_CONV_TUNED", "1") == "1":
     import json as _json
@@ -369,6 +370,6 @@ def conv_op(plan, x, x_shape, w, bias, cout, k, stride, pad, act, y, y_shape, K,
     # arithmetic out of the GEMM loop (measured: GN+ReLU head conv 1.83 -> 1.74 ms); for a plain input
     # the extra pass costs more than the in-loop split (box head 2.48 -> 2.60 ms)
     xf = in_scale is not None or in_shift is not None or in_relu
-    if CONV_PRESPLIT and xf and w3 is not None and C % 32 == 0 and op.i[23] in (0, 25):
+    if CONV_PRESPLIT and (xf or CONV_PRESPLIT == 2) and w3 is not None and C % 32 == 0 and op.i[23] in (0, 25):
         op.p[8] = plan.x3_scratch(3 * B * H * W * C + 32)  # 32 leading zeros (csrc/conv.hip X3Z)
     return plan.add(op)
