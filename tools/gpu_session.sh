@@ -7,9 +7,10 @@ export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 : > gpurun_out/steps.log
 step() {  # step <name> <timeout> <cmd...>: stop the script on anything but success/test-failure
     local name=$1 t=$2; shift 2
+    local t0=$SECONDS
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
-    echo "[$name] rc=$rc" >> gpurun_out/steps.log
+    echo "[$name] rc=$rc ${SECONDS}s-${t0}s = $((SECONDS - t0)) s" >> gpurun_out/steps.log
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
     if grep -q "illegal memory access\|Memory access fault" "gpurun_out/$name.log"; then
         echo "fault in $name: stopping" >> gpurun_out/steps.log; exit 7; fi
