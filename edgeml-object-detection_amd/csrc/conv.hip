@@ -1221,7 +1221,6 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
             mfmas(F);
         }
     };
-    if constexpr (X6B_MF16 && PF != 2 && X6B_PIPE) {
     // 16x16x32 form (X6B_MF16): the wave's 32TM x 32TN tile as (2TM) x (2TN) 16x16 C tiles, each MFMA
     // taking the whole 32-deep stage (lane l: row l & 15, k chunk l >> 4 of the swizzled 64-B row).
     // Under load the chip holds a higher clock for this shape than for 32x32x16 at the same cycles per
@@ -1269,6 +1268,19 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][0], c, 0, 0, 0);
             }
     };
+    // back to the 32x32 block view of the epilogue: block (i, j) register 4(2ii + jj) + r
+    auto epilogue16 = [&]() {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = acc4[2 * i + (q >> 1)][2 * j + (q & 1)][r];
+        conv_epilogue<TM, TN, true>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+    };
+    if constexpr (X6B_MF16 && PF != 2 && X6B_PIPE) {
     Regs r0;
     F16 F0, F1;
     load_stage(r0, next_k(ca), 0);
@@ -1306,16 +1318,7 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
         __syncthreads();
     }
     mfma16(F1, F1, 1, 1);
-    // back to the 32x32 block view of the epilogue: block (i, j) register 4(2ii + jj) + r
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = acc4[2 * i + (q >> 1)][2 * j + (q & 1)][r];
-    conv_epilogue<TM, TN, true>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+    epilogue16();
     return;
     } else if constexpr (PF != 2 && X6B_PIPE) {
     // Skewed pipeline: the second K half of stage k-1 (fragments held in registers across the
@@ -1412,13 +1415,27 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
     __syncthreads();
     auto step = [&](int kc, Regs& hold, Regs& next) {
         if (kc + 2 < nk) load_stage(next, next_k(ca), kc & 1);  // (no LDS-DMA with two register stages)
-        compute(kc & 1);
+        if constexpr (X6B_MF16) {  // the four quadrants of the 16x16x32 form, no carry
+            F16 F0, F1;
+            read16(F0, kc & 1, 0);
+            read16(F1, kc & 1, 1);
+            mfma16(F0, F0, 0, 0);
+            mfma16(F0, F1, 0, 1);
+            mfma16(F1, F0, 1, 0);
+            mfma16(F1, F1, 1, 1);
+        } else {
+            compute(kc & 1);
+        }
         if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
         __syncthreads();
     };
     for (int kc = 0; kc < nk; kc += 2) {
         step(kc, r1, r0);
         if (kc + 1 < nk) step(kc + 1, r0, r1);
+    }
+    if constexpr (X6B_MF16) {
+        epilogue16();
+        return;
     }
     } else {
     Regs r0;
