@@ -896,18 +896,20 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // P1: 1x1, stride 1, dense input (p.lin_x): a stage's k0 is the channel, and rows past M load row 0
 // (their outputs are never stored), so the A loads need no tap or bounds work; with Cin % 32 != 0
 // (!UT) the chunks past Cin are zeroed (they meet the zero weight padding).
-template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF, bool P1 = false>
-__global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
+// BN = 64 (with BM = 128, the skewed 16x16x32 pipeline and LDS-DMA B only): 4 x 2 waves of 32 x 32
+// for the Cout = 64 layers, which a 128-wide N tile computes half empty; waves 0..3 copy the B rows.
+template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF, bool P1 = false, int BN = 128>
+__global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
     static_assert(!P1 || !PS, "pointwise stages: fp32 input");
     constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
-    constexpr int WM = BM == 256 ? 4 : 2, WN = 8 / WM, TM = BM / (WM * 32), TN = 128 / (WN * 32), NT = 512;
-    constexpr int BN = 128;
+    static_assert(BN == 128 || (BN == 64 && BM == 128 && GL && X6B_MF16 && !PS), "x6b BN = 64: 128 x 64, LDS-DMA B, 16x16x32");
+    constexpr int WM = BN == 64 ? 4 : (BM == 256 ? 4 : 2), WN = 8 / WM, TM = BM / (WM * 32), TN = BN / (WN * 32), NT = 512;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
     constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
     constexpr int PA = BM * BK6B, PB = BN * BK6B;  // bf16 elements per plane
-    static_assert(3 * BN * BK6B / 8 == 3 * NT, "one B-plane chunk per thread per plane");
+    static_assert(3 * BN * BK6B / 8 == 3 * NT || BN == 64, "one B-plane chunk per thread per plane");
 
     __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * (PA + PB)];
     unsigned short* As = lds;
@@ -994,7 +996,7 @@ __global__ void __launch_bounds__(512, BM == 64 ? 2 : 1) conv_x6b_kernel(ConvPar
     };
     auto load_part = [&](Regs& R, const StageK& sk, int bbuf, bool la, bool lb) {
         const int k0 = sk.k0;
-        if (GL && lb) {
+        if (GL && lb && 16 * wid < BN) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
             // -> the 16-B slot l of the block); the swizzle is applied on the source address
             const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 2) & 3);
@@ -1498,7 +1500,7 @@ static bool x6b_p1() {
     return v;
 }
 
-template <int BM = 256, int PF = X6B_PF>
+template <int BM = 256, int PF = X6B_PF, int BN = 128>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     const ConvParams& p = p0;
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
@@ -1506,10 +1508,10 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     if (p.ksplit > 1)
         EDGEDET_REQUIRE(p.ksplit == 2 && !p.res && p.act == 0 && p.Kpad >= 2 * BK6B,
                         "conv split-K: 2 halves, no residual, no activation (y must be zeroed)");
-    const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, 128) * (p.ksplit > 1 ? 2 : 1);
+    const int64_t nwg = cdiv(p.M, BM) * cdiv(p.Cout, BN) * (p.ksplit > 1 ? 2 : 1);
     EDGEDET_REQUIRE(nwg < (1ll << 31), "conv grid too large");
     const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
-    if (BM == 256 && x6b_presplit(p)) {
+    if (BM == 256 && BN == 128 && x6b_presplit(p)) {
         const int64_t items = (int64_t)p.B * p.H * p.W * (p.Cin / 8);
         const unsigned g = (unsigned)std::min<int64_t>(cdiv(items, 256), 256 * 64);
         hipLaunchKernelGGL(xf ? split_act_kernel<true> : split_act_kernel<false>, dim3(g), dim3(256), 0, s, p);
@@ -1519,10 +1521,10 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
         return 0;
     }
     const bool p1 = p.lin_x && p.KH == 1 && p.KW == 1 && p.Cin % 4 == 0 && x6b_p1();
-    auto k = p1 ? (xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, true> : conv_x6b_kernel<true, false, false, BM, PF, true>)
-                      : (ut ? conv_x6b_kernel<false, true, false, BM, PF, true> : conv_x6b_kernel<false, false, false, BM, PF, true>))
-         : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF> : conv_x6b_kernel<true, false, false, BM, PF>)
-              : (ut ? conv_x6b_kernel<false, true, false, BM, PF> : conv_x6b_kernel<false, false, false, BM, PF>);
+    auto k = p1 ? (xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, true, BN> : conv_x6b_kernel<true, false, false, BM, PF, true, BN>)
+                      : (ut ? conv_x6b_kernel<false, true, false, BM, PF, true, BN> : conv_x6b_kernel<false, false, false, BM, PF, true, BN>))
+         : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, false, BN> : conv_x6b_kernel<true, false, false, BM, PF, false, BN>)
+              : (ut ? conv_x6b_kernel<false, true, false, BM, PF, false, BN> : conv_x6b_kernel<false, false, false, BM, PF, false, BN>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
     EDGEDET_LAUNCH_CHECK();
     return 0;
@@ -1724,6 +1726,7 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 30: return launch_x6b<128, 2>(p, s);     // the same, two register stages
         case 31: return launch_x6b<64, 1>(p, s);      // 64 x 128, bf16x6, two workgroups per CU
         case 32: return launch_x6b<64, 2>(p, s);      // the same, two register stages
+        case 38: return launch_x6b<128, 1, 64>(p, s); // 128 x 64, bf16x6, 32-deep swizzled stages (Cout <= 64 layers)
         case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
             ConvParams q = p;
             q.ksplit = 2;

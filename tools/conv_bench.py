@@ -22,6 +22,8 @@ SHAPES = {  # name: (B, H, W, Cin, Cout, k, stride)
     "ssd_12_3": (16, 20, 20, 672, 112, 1, 1),
     "retina_cls": (8, 100, 100, 256, 819, 3, 1),
     "ssd_head_cls1b": (16, 10, 10, 480, 546, 1, 1),
+    "layer1_3x3": (8, 200, 200, 64, 64, 3, 1),
+    "layer1_1x1_in": (8, 200, 200, 256, 64, 1, 1),
     "ssd_02_expand": (16, 160, 160, 16, 64, 1, 1),
     "ssd_02_project": (16, 80, 80, 64, 24, 1, 1),
     "ssd_03_expand": (16, 80, 80, 24, 72, 1, 1),
