@@ -958,12 +958,23 @@ class FasterRCNN {
 
     void pack_all() { lower(1, MIN_SIZE, MIN_SIZE, false, true); }
 
+    // [TV] GeneralizedRCNNTransform resize (detect.py:78): the scale is a float32 tensor
+    // op, min(800. / min_f32, 1333. / max_f32), where `float / Tensor` is reciprocal(t) * x; the sizes
+    // are floor(side * double(scale)) (recompute_scale_factor=True). volatile keeps each fp32 rounding.
+    static void resized_size(int H, int W, int& Ho, int& Wo) {
+        volatile float rmin = 1.0f / (float)std::min(H, W), rmax = 1.0f / (float)std::max(H, W);
+        volatile float a = rmin * (float)MIN_SIZE, b = rmax * (float)MAX_SIZE;
+        const double scale = (double)std::min((float)a, (float)b);
+        Ho = (int)std::floor(H * scale);
+        Wo = (int)std::floor(W * scale);
+    }
+
     std::unique_ptr<Plan> lower(int B, int H, int W, bool u8, bool pack_only = false) {
         auto Pp = std::make_unique<Plan>();
         Plan& P = *Pp;
         const int NC = cfg_.num_classes;
-        const double scale = std::min((double)MIN_SIZE / std::min(H, W), (double)MAX_SIZE / std::max(H, W));
-        const int Ho = (int)std::floor(H * scale), Wo = (int)std::floor(W * scale);
+        int Ho, Wo;
+        resized_size(H, W, Ho, Wo);
         const int Hp = (Ho + DIV - 1) / DIV * DIV, Wp = (Wo + DIV - 1) / DIV * DIV;
         const int inp = P.buf({B, 3, H, W}, u8 ? 1 : 4, "images");
         const int x = P.buf({B, Hp, Wp, 4}, 4, "pre");

@@ -8,8 +8,9 @@ read as RGB and scaled by 1/255, every image gets one ``<name[:-4]>.npy`` (N,6) 
 ``[cls, xc, yc, w, h, conf]`` normalised by the original size, rows in score order, an empty result
 still writes a (0,6) file.  Differences: images of equal size are batched across the whole list
 (results are per image and identical to batch=1) and decoded by a thread pool ahead of the engine,
-and under ``torchrun`` the sorted list is split into contiguous shards, one per GPU, with the output
-rows gathered to rank 0 over RCCL (distributed.py).
+and under ``torchrun`` the single-process run's batch list is split into contiguous blocks of
+batches, one per GPU (so every file is byte-identical whatever the GPU count), with the output rows
+gathered to rank 0 over RCCL (distributed.py).
 """
 import argparse
 import os
@@ -86,22 +87,25 @@ def _image_size(path):
         return im.size[1], im.size[0]
 
 
-def _decoded_batches(dataset, batch, workers=None):
-    """Yield (names, (H, W), uint8 [B,3,H,W] pinned batch) for batches of at most `batch` equal-size
-    images: groups by size in first-appearance order, names in sorted order within a group.  Each
-    image is decoded straight into its slot of the batch's pinned buffer (the engine uploads it as
-    is) on a thread pool (one thread per usable host core; PIL releases the GIL while decoding), with
-    the next two batches in flight while the caller uses the current one."""
+def image_sizes(dataset, workers=None):
+    """(H, W) of every image of the dataset, from the file headers (no decode), on a thread pool."""
+    import concurrent.futures as cf
+    from .distributed import usable_cpus
+    paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
+    with cf.ThreadPoolExecutor(workers or usable_cpus()) as ex:
+        return list(ex.map(_image_size, paths))
+
+
+def _decoded_batches(dataset, chunks, sizes, workers=None):
+    """Yield (names, (H, W), uint8 [B,3,H,W] pinned batch) for the given batches of equal-size images
+    (lists of dataset indices, distributed.size_batches).  Each image is decoded straight into its
+    slot of the batch's pinned buffer (the engine uploads it as is) on a thread pool (one thread per
+    usable host core; PIL releases the GIL while decoding), with the next two batches in flight while
+    the caller uses the current one."""
     import concurrent.futures as cf
     from .distributed import usable_cpus
     workers = workers or usable_cpus()
-    paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
     with cf.ThreadPoolExecutor(workers) as ex:
-        sizes = list(ex.map(_image_size, paths))
-        groups = {}
-        for i, hw in enumerate(sizes):
-            groups.setdefault(hw, []).append(i)
-        chunks = [idx[k:k + batch] for idx in groups.values() for k in range(0, len(idx), batch)]
         pin = torch.cuda.is_available()
 
         def sub(c):  # one future per image, so a batch decodes on many threads at once
@@ -137,8 +141,7 @@ def main(opts):
     if not torch.cuda.is_available():
         raise RuntimeError("edgeml_amd.detect needs an MI355X (HIP) device; there is no CPU path")
     rank, world = dist_mod.ensure_initialized()
-    my_names = dist_mod.shard(img_names, rank, world)
-    dataset = ObjectDetectionDataset(opts.img_dir, my_names)
+    dataset = ObjectDetectionDataset(opts.img_dir, img_names)
     num_class = 91 if opts.dataset == "coco" else 21
     device = f"cuda:{dist_mod.device_index()}"
     torch.cuda.set_device(device)
@@ -149,16 +152,23 @@ def main(opts):
     Path(opts.save_dir).mkdir(parents=True, exist_ok=True)
     batch = min(getattr(opts, "batch", None) or model.max_batch, model.max_batch)
     results = {}
-    # Batches of equal-size images across the whole shard (sizes from the file headers, no decode),
-    # decoded by a thread pool one batch ahead of the engine (PIL releases the GIL while decoding).
-    # Up to model.INFLIGHT batches on the device at once (run_batches), so one batch's NMS tail
-    # overlaps the next batch's backbone.
-    tagged = (((names, hw), buf) for names, hw, buf in _decoded_batches(dataset, batch))
+    # Batches of equal-size images across the whole list (sizes from the file headers, no decode),
+    # formed exactly as a single-process run forms them; under torchrun each rank takes a contiguous
+    # block of those batches, so outputs are independent of the GPU count.  Decoded by a thread pool
+    # one batch ahead of the engine (PIL releases the GIL while decoding).  Up to model.INFLIGHT
+    # batches on the device at once (run_batches), so one batch's NMS tail overlaps the next
+    # batch's backbone.
+    sizes = image_sizes(dataset)
+    chunks = dist_mod.size_batches(sizes, batch)
+    shards = [dist_mod.batch_shard(chunks, r, world) for r in range(world)]
+    shard_names = [[img_names[i] for c in sh for i in c] for sh in shards]
+    my_names = shard_names[rank]
+    tagged = (((names, hw), buf) for names, hw, buf in _decoded_batches(dataset, shards[rank], sizes))
     for (names, (h, w)), counts, boxes, scores, labels in model.run_batches(tagged, raw=True):
         for name, rows in zip(names, fmt.format_batch(boxes, scores, labels, counts, h, w, opts.dataset)):
             results[name] = rows
     if world > 1:
-        results = dist_mod.gather_rows(results, my_names, img_names, rank, world)
+        results = dist_mod.gather_rows(results, my_names, img_names, rank, world, shards=shard_names)
     if rank == 0:
         for name in img_names:
             fmt.save_npy(opts.save_dir, name, results[name])

@@ -1,8 +1,11 @@
 """One process per GPU: contiguous shards of the sorted image list and a gather of the output rows.
 
-SURVEY.md §8e: images are independent, so rank r processes the contiguous block
-[r*N//world, (r+1)*N//world) of sorted(os.listdir(img_dir)) (detect.py:64) with no collective on the
-data path.  The only exchange is the final gather of the per-image (n_i, 6) float64 rows to rank 0,
+SURVEY.md §8e: images are independent, so the ranks split sorted(os.listdir(img_dir)) (detect.py:64)
+with no collective on the data path.  The detect CLI shards at BATCH granularity: every rank forms
+the single-process run's list of size-grouped batches (size_batches) and takes a contiguous block of
+it (batch_shard), so each image runs in exactly the batch it would run in on one GPU and its output
+bits do not depend on the GPU count (the conv tile table is keyed on the batch size).  The reward CLI
+shards target images as contiguous blocks (shard).  The only exchange is the final gather of the per-image (n_i, 6) float64 rows to rank 0,
 which writes every file (single writer): an all_gather of per-rank row counts, then an all_gather of
 the packed rows padded to the largest rank (``torch.distributed``; backend "nccl" = RCCL over xGMI on
 the MI355X node, "gloo" in the CPU tests).
@@ -72,8 +75,33 @@ def shard(items, rank, world):
     return list(items)[lo:hi]
 
 
-def gather_rows(results, my_names, all_names, rank, world, device=None):
-    """results: {name: (n,6) float64} for this rank's shard -> {name: rows} for every image on rank 0."""
+def size_batches(sizes, batch):
+    """The single-process detect run's batches (detect.py:64-66 order, batched): images grouped by
+    (H, W) in order of first appearance, each group cut into chunks of at most `batch` in sorted-name
+    order.  sizes: [(H, W)] per image of the sorted list -> [[image index, ...], ...]."""
+    groups = {}
+    for i, hw in enumerate(sizes):
+        groups.setdefault(tuple(hw), []).append(i)
+    return [idx[k:k + batch] for idx in groups.values() for k in range(0, len(idx), batch)]
+
+
+def batch_shard(chunks, rank, world):
+    """A contiguous block of the batch list for `rank`, balanced by image count: batch j goes to
+    rank floor(c_j * world / N), c_j = the images in the batches before it.  Every batch lands on
+    exactly one rank, unchanged, so per-image results equal the world-1 run's bit for bit."""
+    n = sum(len(c) for c in chunks)
+    out, start = [], 0
+    for c in chunks:
+        if min(world - 1, start * world // max(n, 1)) == rank:
+            out.append(c)
+        start += len(c)
+    return out
+
+
+def gather_rows(results, my_names, all_names, rank, world, device=None, shards=None):
+    """results: {name: (n,6) float64} for this rank's shard -> {name: rows} for every image on rank 0.
+    shards: the names of every rank's shard in its processing order (all ranks pass the same list);
+    None means the contiguous blocks of `all_names` that shard() gives."""
     if world == 1:
         return results
     if not dist.is_initialized():
@@ -100,8 +128,11 @@ def gather_rows(results, my_names, all_names, rank, world, device=None):
         return None
     out = {}
     for k in range(world):
-        lo, hi = shard_bounds(len(all_names), k, world)
-        names = all_names[lo:hi]
+        if shards is None:
+            lo, hi = shard_bounds(len(all_names), k, world)
+            names = all_names[lo:hi]
+        else:
+            names = shards[k]
         cnt = cs[k].cpu().numpy()[:len(names)]
         rr = rs[k].cpu().numpy()
         pos = 0

@@ -625,7 +625,13 @@ class FasterRCNNFPNv2(_Detector):
 
 
     def resized_size(self, H, W):
-        scale = min(float(self.MIN_SIZE) / min(H, W), float(self.MAX_SIZE) / max(H, W))
+        """[TV] GeneralizedRCNNTransform resize (detect.py:78): the scale is a float32
+        tensor op, `min(800. / min_f32, 1333. / max_f32)` with `float / Tensor` = `reciprocal(t) * x`;
+        the sizes are `floor(side * float(scale))` in double (`recompute_scale_factor=True`)."""
+        f32 = np.float32
+        a = f32(f32(1.0) / f32(min(H, W))) * f32(self.MIN_SIZE)
+        b = f32(f32(1.0) / f32(max(H, W))) * f32(self.MAX_SIZE)
+        scale = float(min(a, b))
         return int(math.floor(H * scale)), int(math.floor(W * scale))
 
     def _lower_body(self, P, B, H, W, u8=False):

@@ -146,10 +146,22 @@ def remove_small(boxes, min_size):
 
 
 # ---------------------------------------------------------------- transform (SURVEY A.0 "Transform resize")
+def resize_scale_f32(h, w, min_size, max_size):
+    """[TV] `_resize_image_and_masks`: `scale = torch.min(800. / min_f32, 1333. / max_f32)` on float32
+    tensors. `float / Tensor` is `Tensor.__rtruediv__` = `reciprocal(t) * other`, so
+    each ratio is fp32(fp32(1/side) * size); `.item()` widens the smaller one to a Python double."""
+    mn, mx = np.float32(min(h, w)), np.float32(max(h, w))
+    a = np.float32(np.float32(1.0) / mn) * np.float32(min_size)
+    b = np.float32(np.float32(1.0) / mx) * np.float32(max_size)
+    return float(min(a, b))
+
+
 def resize_output_size(h, w, min_size, max_size, fixed=None):
+    """F.interpolate(scale_factor=s, recompute_scale_factor=True): size = floor(float(side) * s) in
+    double, s the fp32 scale above."""
     if fixed is not None:
         return fixed
-    scale = min(float(min_size) / min(h, w), float(max_size) / max(h, w))
+    scale = resize_scale_f32(h, w, min_size, max_size)
     return int(math.floor(h * scale)), int(math.floor(w * scale))
 
 

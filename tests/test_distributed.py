@@ -23,13 +23,20 @@ def _rows_for(name):
     return rs.rand(n, 6)
 
 
-def _worker(rank, world, port, names, q):
+def _worker(rank, world, port, names, q, batched=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from edgeml_amd import distributed as D
-    mine = D.shard(names, rank, world)
+    shards = None
+    if batched:  # the detect CLI's batch-granular shards: two sizes, batches of 3
+        sizes = [(480, 640) if int(n) % 3 else (427, 640) for n in names]
+        chunks = D.size_batches(sizes, 3)
+        shards = [[names[i] for c in D.batch_shard(chunks, r, world) for i in c] for r in range(world)]
+        mine = shards[rank]
+    else:
+        mine = D.shard(names, rank, world)
     res = {n: _rows_for(n) for n in mine}
-    out = D.gather_rows(res, mine, names, rank, world)
+    out = D.gather_rows(res, mine, names, rank, world, shards=shards)
     if rank == 0:
         q.put({k: v.tolist() for k, v in out.items()})
     dist.barrier()
@@ -45,13 +52,33 @@ def test_shard_is_contiguous_partition():
         assert max(map(len, parts)) - min(map(len, parts)) <= 1
 
 
-@pytest.mark.parametrize("n", [7, 1])
-def test_gather_rows_world2(n):
+def test_size_batches_and_batch_shard():
+    """Batch-granular shards: every rank's batches are the world-1 batches, unchanged, in a
+    contiguous block of the world-1 order, balanced by image count."""
+    from edgeml_amd import distributed as D
+    rs = np.random.RandomState(0)
+    pool = [(480, 640), (640, 480), (427, 640), (612, 612)]
+    for n, batch in ((103, 8), (5000, 32), (7, 32), (40, 1), (0, 4)):
+        sizes = [pool[k] for k in rs.randint(0, 4, n)]
+        chunks = D.size_batches(sizes, batch)
+        assert sorted(i for c in chunks for i in c) == list(range(n))
+        for c in chunks:
+            assert len(c) <= batch and len({sizes[i] for i in c}) == 1 and c == sorted(c)
+        for world in (1, 2, 3, 8):
+            parts = [D.batch_shard(chunks, r, world) for r in range(world)]
+            assert sum(parts, []) == chunks  # contiguous blocks, world-1 order, batches unchanged
+            if n >= world * batch * 4:
+                load = [sum(map(len, p)) for p in parts]
+                assert max(load) - min(load) <= 2 * batch
+
+
+@pytest.mark.parametrize("n,batched", [(7, False), (1, False), (11, True)])
+def test_gather_rows_world2(n, batched):
     names = [f"{i:06d}" for i in range(n)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, names, q, batched)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

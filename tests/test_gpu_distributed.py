@@ -7,9 +7,10 @@ file, then each rank evaluates its block of target images and rank 0 gathers the
 (reward.py:78-92).  Both ranks share cuda:0 over the gloo backend (the box has one GPU; on an
 8-GPU node the same code binds LOCAL_RANK's device and uses nccl = RCCL).  Every output file must
 be byte-identical to a single-process run.  Per-image results depend on the batch an image runs
-in (the conv tile choice is keyed on the batch size), so the cases fix the batch so that both runs
-form the same batches: 8 equal-size images at --batch 2 (shards of 4 + 4), and a ragged 7-image
-set at --batch 1 (shards of 4 + 3).
+in (the conv tile choice is keyed on the batch size), so detect shards at batch granularity
+(distributed.size_batches / batch_shard): each rank runs a contiguous block of exactly the batches
+the single-process run forms.  The cases use the CLI's default --batch (SSD 32, FRCNN 8) on ragged,
+mixed-size sets, plus a forced small batch that splits a size group across the ranks.
 """
 import os
 import socket
@@ -35,7 +36,8 @@ def _run_cli(img, lab, work, E, batch):
     import torch.distributed as dist
     from edgeml_amd import detect, reward
     for stage, model in (("weak", "ssd"), ("strong", "faster_rcnn")):
-        detect.main(detect.getargs([img, os.path.join(work, stage), "--model", model, "--batch", str(batch)]))
+        extra = ["--batch", str(batch)] if batch else []  # 0: the CLI default (model.max_batch)
+        detect.main(detect.getargs([img, os.path.join(work, stage), "--model", model, *extra]))
         if dist.is_initialized():
             dist.barrier()  # rank 0 has written every file before any rank reads them
     reward.main(reward.getargs([os.path.join(work, "weak"), os.path.join(work, "strong"), lab,
@@ -57,14 +59,18 @@ def _rank(rank, world, port, img, lab, work, E, batch, q):
         raise
 
 
-@pytest.mark.parametrize("n,batch", [(8, 2), (7, 1)])
-def test_detect_and_reward_world2_equal_world1(n, batch):
+@pytest.mark.parametrize("n,batch,sizes", [
+    (13, 0, [(480, 640), (427, 640)]),     # default batch, two size groups of ragged length
+    (21, 0, [(480, 640), (640, 640)]),     # default batch: FRCNN's 8 cuts each group into 8 + rest
+    (9, 2, [(480, 640), (375, 500)]),      # small batches: a size group straddles the ranks
+])
+def test_detect_and_reward_world2_equal_world1(n, batch, sizes):
     from edgeml_amd import synthetic
     warnings.filterwarnings("ignore")
     E = 4
     with tempfile.TemporaryDirectory() as td:
         img, lab = os.path.join(td, "imgs"), os.path.join(td, "labels")
-        synthetic.make_dataset(img, n, seed=5, label_dir=lab, sizes=[(480, 640)])
+        synthetic.make_dataset(img, n, seed=5, label_dir=lab, sizes=sizes)
         one, two = os.path.join(td, "w1"), os.path.join(td, "w2")
         ctx = mp.get_context("spawn")
         q = ctx.Queue()

@@ -46,12 +46,21 @@ def test_ssd_detections_match_oracle(ssd, h, w, n):
     assert rep["rows"] > 0
 
 
-@pytest.mark.parametrize("h,w,n", [(640, 640, 1), (480, 640, 2)])
+# 427x640, 375x500 and 333x500 resize to 799 rows under the fp32 scale rule of [TV]'s transform
+#  and to 800 under a double one: the plan's size is checked against the oracle's
+# transform inside frcnn_check, and the expected size is pinned here.
+RESIZED = {(427, 640): (799, 1199), (375, 500): (799, 1066), (333, 500): (799, 1201)}
+
+
+@pytest.mark.parametrize("h,w,n", [(640, 640, 1), (480, 640, 2), (427, 640, 1), (375, 500, 2)])
 def test_frcnn_detections_match_oracle(frcnn, h, w, n):
     from edgeml_amd import synthetic
     sd, model = frcnn
     imgs = synthetic.make_batch(n, h, w, seed=31 + h)
-    rep = PM.frcnn_check(_run(model, imgs), sd, 91, imgs, f"frcnn {n}x{h}x{w}")
+    plan = _run(model, imgs)
+    if (h, w) in RESIZED:
+        assert tuple(plan.resized[:2]) == RESIZED[(h, w)]
+    rep = PM.frcnn_check(plan, sd, 91, imgs, f"frcnn {n}x{h}x{w}")
     print(rep)
     assert rep["box"]["rows"] > 0
 

@@ -138,7 +138,7 @@ def test_retinanet_postprocess_on_identical_heads(retina):
         assert n > 0
 
 
-@pytest.mark.parametrize("h,w,n", [(480, 640, 1), (640, 640, 2)])
+@pytest.mark.parametrize("h,w,n", [(480, 640, 1), (640, 640, 2), (427, 640, 1), (375, 500, 1)])
 def test_retinanet_detections_match_oracle(retina, h, w, n):
     from edgeml_amd import synthetic
     from tests import parity_models as PM

@@ -23,6 +23,7 @@ CASES = [
     ("ssd", 21, False, 3, 427, 640, False),   # full tail, VOC classes
     ("faster_rcnn", 91, True, 1, 480, 640, False),
     ("faster_rcnn", 21, True, 2, 612, 612, True),
+    ("faster_rcnn", 91, True, 1, 427, 640, True),  # fp32 resize scale: 799 x 1199
 ]
 
 
