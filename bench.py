@@ -5,7 +5,9 @@
 A step = one forward of the detector over one batch of synthetic 640x640 images already resident in
 HBM (preprocess -> backbone -> heads -> decode -> NMS -> final top-k), replayed from a captured
 hipGraph, plus the D2H copy of the batch's detections (counts, boxes, scores, labels) into pinned
-host memory.  N=1 workload: SSDLite320-MobileNetV3 at batch 32 (configs[1]); FRCNN-R50-FPN-v2 at
+host memory.  The steps rotate over the model's INFLIGHT independent plan instances
+(SSDLite 4, FRCNN 2: the counts the detect CLI's run_batches keeps on the device); the SSD rate at
+the other count is reported beside it ("alt_inflight").  N=1 workload: SSDLite320-MobileNetV3 at batch 32 (configs[1]); FRCNN-R50-FPN-v2 at
 batch 8 (configs[2]) is measured beside it and reported under "frcnn".  For N>1 the script is
 launched by torch.distributed.run: one process per GPU, each replays its own batch (weak scaling:
 images are independent, no collective on the data path); the timed region is bracketed by a
@@ -35,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SSD_BYTES_PER_IMG = 87.1e6   # algorithmic HBM bytes per SSDLite image
 FP32_MFMA_PEAK_TFS = 157.3   # dense fp32 MFMA (= fp32 vector peak)
 
 
@@ -236,7 +239,7 @@ def op_work(op):
         return "retina_select", 0.0, 4.0 * i[0] * n * (i[3] + 4)
     if k == O.RETINA_CLASS_NMS:
         return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
-    if k in (O.FORK, O.JOIN):
+    if k in (O.FORK, O.JOIN, O.WAIT):
         return "lanes", 0.0, 0.0
     if k == O.MEMSET:  # zeroing the output of a split-K conv
         return "conv", 0.0, float(i[0])
@@ -255,7 +258,7 @@ def per_op_times(plan, stream, reps=20):
     recs["i"][:, O.LANE_FIELD] = 0  # time every op alone on the timed stream
     with torch.cuda.stream(stream):
         for k in range(len(recs)):
-            if recs[k]["kind"] in (O.FORK, O.JOIN):
+            if recs[k]["kind"] in (O.FORK, O.JOIN, O.WAIT):
                 res.append(0.0)
                 continue
             ptr = recs[k:k + 1].ctypes.data_as(ctypes.c_void_p)
@@ -353,18 +356,24 @@ def _cpu_model():
     return None
 
 
-def orie_vs_ref(n=6, E=5):
-    """ORIE of the engine's files vs ORIE of the CPU oracle's files on n synthetic images (SSDLite
-    weak, FRCNN strong; pseudo ground truth = the oracle strong detector's confident boxes): the
-    engine side goes through the product consumer (GPU reward), the reference side through the
-    oracle consumer (oracle/orie.py, pinned to the reference's own G2 values)."""
+def orie_vs_ref(n=48, E=None):
+    """ORIE of the engine's files vs ORIE of the CPU oracle's files on n synthetic 640x640 images
+    (SSDLite weak, FRCNN strong; pseudo ground truth = the oracle strong detector's confident boxes),
+    E = n - 1 so every image is in every ensemble, as in config 4 (E = 1000 over 5,000): the engine
+    side goes through the product consumer (GPU reward), the reference side through the oracle
+    consumer (oracle/orie.py, pinned to the reference's own G2 values).  The oracle's batch=1 CPU
+    forwards are timed on the way: they are the FRCNN cpu_baseline (same images, same loop)."""
     import tempfile
     import warnings
     from edgeml_amd import fmt, models, reward, synthetic
     from oracle import orie
     from oracle.frcnn import FasterRCNNOracle
     from oracle.ssdlite import SSDLiteOracle
+    from edgeml_amd.distributed import usable_cpus
     warnings.filterwarnings("ignore")
+    torch.set_num_threads(usable_cpus())
+    E = n - 1 if E is None else E
+    cpu_s = {"weak": 0.0, "strong": 0.0}
     sd_w, sd_s = synthetic.synthetic_state_dict("ssd", 91, True), synthetic.synthetic_state_dict("faster_rcnn", 91)
     eng = {"weak": models.SSDLite320(sd_w, 91, True).to("cuda"), "strong": models.FasterRCNNFPNv2(sd_s, 91).to("cuda")}
     ref = {"weak": SSDLiteOracle(sd_w, 91, True), "strong": FasterRCNNOracle(sd_s, 91)}
@@ -379,7 +388,10 @@ def orie_vs_ref(n=6, E=5):
                 p = eng[tag](img.cuda())[0]
                 fmt.save_npy(d("eng_" + tag), name, fmt.format_detections(
                     p["boxes"].cpu().numpy(), p["scores"].cpu().numpy(), p["labels"].cpu().numpy(), 640, 640))
+                t0 = time.perf_counter()
                 q = ref[tag]([img[0]])[0]
+                if i:  # image 0 warms the oracle up
+                    cpu_s[tag] += time.perf_counter() - t0
                 rows = fmt.format_detections(q["boxes"].numpy(), q["scores"].numpy(), q["labels"].numpy(), 640, 640)
                 fmt.save_npy(d("ref_" + tag), name, rows)
                 if tag == "strong":
@@ -389,8 +401,14 @@ def orie_vs_ref(n=6, E=5):
         wd, sd, lab = reward.set_data(d("eng_weak"), d("eng_strong"), d("labels"))
         got = reward.compute_orie_all(wd, sd, lab, E, seed=1000)
         want = orie.orie_all(d("ref_weak"), d("ref_strong"), d("labels"), E, seed=1000)
-    return {"max_abs_diff": float(np.abs(got - want).max()), "images": n, "num_ensemble": E,
-            "nonzero_ref": int(np.count_nonzero(want))}
+    d = np.abs(got - want)
+    out = {"max_abs_diff": float(d.max()), "images": n, "num_ensemble": E,
+           "images_differing": int(np.count_nonzero(d)), "nonzero_ref": int(np.count_nonzero(want))}
+    frcnn_cpu = {"value": round((n - 1) / cpu_s["strong"], 3), "unit": "images/s", "cores": torch.get_num_threads(),
+                 "kind": "port", "host_cores": os.cpu_count(), "host_cpu": _cpu_model(),
+                 "sample": f"{n - 1} synthetic 640x640 images, batch=1 ({cpu_s['strong']:.1f}s), frcnn CPU oracle "
+                           f"(PyTorch-CPU + C restatement of the torchvision eval path), the orie leg's strong pass"}
+    return out, frcnn_cpu
 
 
 def cpu_baseline(kind, budget_s=15.0):
@@ -429,9 +447,11 @@ def main():
     ap.add_argument("--ssd-batch", type=int, default=32)
     ap.add_argument("--frcnn-batch", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="independent plan instances the steps rotate over (batches in flight per GPU)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="independent plan instances the steps rotate over (batches in flight per GPU); "
+                         "0 = the model's INFLIGHT, the count the detect CLI's run_batches keeps in flight")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true", help="skip the SSD rate at the other in-flight count")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dump-ops", default="", help="write the per-op device times of each model to this JSON")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host uint8 -> rows) rates")
@@ -449,11 +469,22 @@ def main():
         plan = m.plan(B, 640, 640)
         plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank).cuda())
         plan.capture(stream)
-        extra = inflight_instances(m, B, args.inflight, 100 * rank)
+        nin = args.inflight or m.INFLIGHT
+        extra = inflight_instances(m, B, nin, 100 * rank)
         el = timed_steps(plan, stream, args.steps, args.warmup, dist, extra)
-        del extra
         out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
-                      "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
+                      "inflight": nin, "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
+        # SURVEY §8(d)'s binding roof for C2: 87.1 MB of algorithmic HBM traffic per image
+        gbs = SSD_BYTES_PER_IMG * out["ssd"]["value"] / world / 1e9
+        out["ssd"]["step_hbm"] = {"bytes_per_img": SSD_BYTES_PER_IMG, "achieved_GBps": round(gbs, 1),
+                                  "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if not args.no_alt:  # the other in-flight count, same plans (reported beside the headline)
+            alt = 2 if nin != 2 else 4
+            more = inflight_instances(m, B, alt - nin + 1, 100 * rank + 7) if alt > nin else []
+            el2 = timed_steps(plan, stream, args.steps, args.warmup, dist, (extra + more)[:alt - 1])
+            del more
+            out["ssd"]["alt_inflight"] = {"inflight": alt, "value": round(world * B * args.steps / el2, 2)}
+        del extra
         if rank == 0 and not args.no_roofline:
             out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps, "ssd")
             attach_traffic(out["ssd"]["roofline"], "ssd")
@@ -469,8 +500,8 @@ def main():
         plan = m.plan(B, 640, 640)
         plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 70).cuda())
         plan.capture(stream)
-        steps = max(2, args.steps // 10)
-        extra = inflight_instances(m, B, args.inflight, 100 * rank + 70)
+        steps = max(20, args.steps // 10)
+        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 70)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
         out["retinanet"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
@@ -484,8 +515,8 @@ def main():
         plan = m.plan(B, 640, 640)
         plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 50).cuda())
         plan.capture(stream)
-        extra = inflight_instances(m, B, args.inflight, 100 * rank + 50)
-        steps = max(2, args.steps // 10)  # FRCNN steps are ~20x SSD's: about a second of timed work
+        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 50)
+        steps = max(20, args.steps // 10)  # FRCNN steps are ~20x SSD's: at least 20 (about half a second)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
         R = float(plan.proposal_count.tensor().float().mean().item())
@@ -520,7 +551,7 @@ def main():
                                 "frcnn": "fasterrcnn_resnet50_fpn_v2 b=%d 640x640 (configs[2])",
                                 "retinanet": "retinanet_resnet50_fpn_v2 b=%d 640x640"}[primary] % p["batch"],
                    "global_batch": p["batch"] * world, "parallelism": f"dp{world}",
-                   "batches_in_flight": args.inflight,
+                   "batches_in_flight": p.get("inflight", args.inflight),
                    "conv_math": plan_mod.CONV_MATH,
                    "weights": "seeded synthetic (COCO weights need a download)"},
     }
@@ -540,11 +571,14 @@ def main():
     line["dets_per_img"] = p.get("dets_per_img")
     if "end_to_end" in p:
         line["end_to_end"] = p["end_to_end"]
+    for k in ("step_hbm", "alt_inflight"):
+        if k in p:
+            line[k] = p[k]
     if not args.no_cpu:
-        line["orie"] = orie_vs_ref()
+        line["orie"], frcnn_cpu = orie_vs_ref()
         line["cpu_baseline"] = cpu_baseline(primary, args.cpu_budget)
         if "frcnn" in out and primary == "ssd":
-            line["frcnn"]["cpu_baseline"] = cpu_baseline("frcnn", args.cpu_budget)
+            line["frcnn"]["cpu_baseline"] = frcnn_cpu
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -1676,15 +1676,11 @@ int merge_topk_launch(const MergeParams& P, int B, hipStream_t s) {
     return 0;
 }
 
-}  // namespace edgedet
-
-using namespace edgedet;
-
-extern "C" int edgedet_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, int64_t n,
-                                   double iou_threshold, int64_t* keep, int32_t* d_num_keep, void* stream) {
-    EDGEDET_REQUIRE(n >= 0 && n <= 1024, "batched_nms: n must be in [0, 1024]");
+// the single-workgroup path of the unit NMS (csrc/unitops.hip: edgedet_nms / edgedet_batched_nms)
+int unit_small_nms(const float* boxes, const float* scores, const int64_t* idxs, int64_t n, double iou_threshold,
+                   int64_t* keep, int32_t* d_num_keep, hipStream_t s) {
+    EDGEDET_REQUIRE(n >= 0 && n <= 1024, "batched_nms: single-workgroup path takes n <= 1024");
     EDGEDET_REQUIRE(d_num_keep && (n == 0 || (boxes && scores && keep)), "batched_nms: null pointer");
-    hipStream_t s = (hipStream_t)stream;
     if (n == 0) {
         EDGEDET_CHECK_HIP(hipMemsetAsync(d_num_keep, 0, sizeof(int32_t), s));
         return 0;
@@ -1699,7 +1695,4 @@ extern "C" int edgedet_batched_nms(const float* boxes, const float* scores, cons
     return 0;
 }
 
-extern "C" int edgedet_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold, int64_t* keep,
-                           int32_t* d_num_keep, void* stream) {
-    return edgedet_batched_nms(boxes, scores, nullptr, n, iou_threshold, keep, d_num_keep, stream);
-}
+}  // namespace edgedet

@@ -53,8 +53,11 @@
 //   RETINA_CLASS_NMS p0..4 level records (box,score,tb,label,count); p5..9 class records [B,K,kmax];
 //                  i0..4 B,L,kin,K,kmax; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
+//   WAIT           lane i0 waits for everything issued so far on lane i1 (both forked, or 0)
 #include <cstdlib>
+#include <memory>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include <map>
@@ -423,73 +426,161 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
     }
 }
 
-// Side streams and fork/join events, created once per (thread, device, caller stream) and reused by
-// every call on that stream: two plans in flight on two caller streams (run_batches) get disjoint
-// side lanes, so their lane work overlaps instead of queueing on one shared side stream.
+// Side streams and fork/join/wait events, one set per (device, caller stream), shared by every
+// thread (cgo and other foreign hosts call from arbitrary OS threads): two plans in flight on two
+// caller streams (run_batches) get disjoint side lanes, so their lane work overlaps instead of
+// queueing on one shared side stream.  The cache is bounded (LANE_CACHE sets, least recently used
+// evicted; edgedet_release_lanes drops a stream's set at once); a set is destroyed when the last run
+// using it returns.  Every WAIT record of a run gets its own event (no event is re-recorded while a
+// wait on it may be pending in the same capture).
 struct Lanes {
     hipStream_t side[EDGEDET_MAX_LANES] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t join_ev[EDGEDET_MAX_LANES] = {};
+    std::vector<hipEvent_t> wait_ev;
+    uint64_t last_use = 0;
+    ~Lanes() {
+        for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
+            if (side[l]) (void)hipStreamDestroy(side[l]);
+            if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
+        }
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        for (hipEvent_t e : wait_ev) (void)hipEventDestroy(e);
+    }
+    bool ensure_wait_events(size_t n) {
+        while (wait_ev.size() < n) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+            wait_ev.push_back(e);
+        }
+        return true;
+    }
 };
-static thread_local std::map<std::pair<int, hipStream_t>, Lanes> g_lanes_by_stream;
+constexpr size_t LANE_CACHE = 16;
+static std::mutex g_lanes_mu;
+static std::map<std::pair<int, hipStream_t>, std::shared_ptr<Lanes>> g_lanes_by_stream;
+static uint64_t g_lanes_clock = 0;
 
-static Lanes* lanes_for(hipStream_t caller) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    auto key = std::make_pair(dev, caller);
-    auto it = g_lanes_by_stream.find(key);
-    if (it != g_lanes_by_stream.end()) return &it->second;
-    Lanes L;
+static std::shared_ptr<Lanes> make_lanes() {
+    auto L = std::make_shared<Lanes>();  // a partial set is destroyed by ~Lanes on the failure paths
     for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
-        if (hipStreamCreateWithFlags(&L.side[l], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&L.join_ev[l], hipEventDisableTiming) != hipSuccess)
+        if (hipStreamCreateWithFlags(&L->side[l], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L->join_ev[l], hipEventDisableTiming) != hipSuccess)
             return nullptr;
     }
-    if (hipEventCreateWithFlags(&L.fork_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
-    return &(g_lanes_by_stream[key] = L);
+    if (hipEventCreateWithFlags(&L->fork_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return L;
 }
 
-static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
+static std::shared_ptr<Lanes> lanes_for(hipStream_t caller) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const auto key = std::make_pair(dev, caller);
+    std::lock_guard<std::mutex> lock(g_lanes_mu);
+    auto it = g_lanes_by_stream.find(key);
+    if (it != g_lanes_by_stream.end()) {
+        it->second->last_use = ++g_lanes_clock;
+        return it->second;
+    }
+    auto L = make_lanes();
+    if (!L) return nullptr;
+    if (g_lanes_by_stream.size() >= LANE_CACHE) {  // evict the least recently used set
+        auto lru = g_lanes_by_stream.begin();
+        for (auto i = g_lanes_by_stream.begin(); i != g_lanes_by_stream.end(); ++i)
+            if (i->second->last_use < lru->second->last_use) lru = i;
+        g_lanes_by_stream.erase(lru);  // destroyed now, or when a run still holding it returns
+    }
+    L->last_use = ++g_lanes_clock;
+    g_lanes_by_stream[key] = L;
+    return L;
+}
+
+static size_t lane_cache_size() {
+    std::lock_guard<std::mutex> lock(g_lanes_mu);
+    return g_lanes_by_stream.size();
+}
+
+// Lane topology of a record sequence, checked before anything is issued (so a refused plan leaves
+// the streams, and a capture, untouched): every op runs on lane 0 or a forked side lane; FORK opens
+// 1..3 side lanes from lane 0 (none open), JOIN closes them into lane 0; WAIT (lane i0 waits for
+// everything issued so far on lane i1) connects two distinct open lanes.  Returns the WAIT count.
+static int64_t check_topology(const edgedet_op* ops, int64_t n) {
+    int forked = 0;
+    int64_t waits = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        const edgedet_op& o = ops[k];
+        const std::string at = "op " + std::to_string(k) + ": ";
+        if (o.kind == EDGEDET_OP_FORK) {
+            EDGEDET_REQUIRE(forked == 0, at + "fork while side lanes are open");
+            EDGEDET_REQUIRE(o.i[0] >= 1 && o.i[0] < EDGEDET_MAX_LANES, at + "fork: 1..3 side lanes");
+            forked = (int)o.i[0];
+        } else if (o.kind == EDGEDET_OP_JOIN) {
+            EDGEDET_REQUIRE(o.i[0] >= 1 && o.i[0] < EDGEDET_MAX_LANES && o.i[0] == forked,
+                            at + "join: the forked side lanes");
+            forked = 0;
+        } else if (o.kind == EDGEDET_OP_WAIT) {
+            const int64_t a = o.i[0], b = o.i[1];
+            EDGEDET_REQUIRE(a >= 0 && b >= 0 && a != b && a <= forked && b <= forked,
+                            at + "wait: two distinct forked lanes");
+            ++waits;
+        } else {
+            const int64_t lane = o.i[EDGEDET_OP_LANE];
+            EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
+                            at + "op on a lane that is not forked");
+        }
+    }
+    EDGEDET_REQUIRE(forked == 0, "plan ends with side lanes still forked (missing JOIN)");
+    return waits;
+}
+
+// own: the lane set to issue on (a graph capture passes its own, see edgedet_graph_create); null = the
+// cached set of the caller stream.
+static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s, std::shared_ptr<Lanes> own = nullptr) {
+    const int64_t waits = check_topology(ops, n);
+    if (waits < 0) return (int)waits;
     bool need_lanes = false;
     for (int64_t k = 0; k < n && !need_lanes; ++k)
         need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
-    Lanes* lanes = need_lanes ? lanes_for(s) : nullptr;
+    std::shared_ptr<Lanes> lanes = !need_lanes ? nullptr : own ? own : lanes_for(s);
     EDGEDET_REQUIRE(!need_lanes || lanes, "could not create the side lanes (streams / events)");
-    int forked = 0;
+    EDGEDET_REQUIRE(!waits || lanes->ensure_wait_events((size_t)waits), "could not create the wait events");
+    auto lane_stream = [&](int64_t l) { return l == 0 ? s : lanes->side[l]; };
+    int64_t wait_k = 0;
     for (int64_t k = 0; k < n; ++k) {
         const edgedet_op& o = ops[k];
         int rc = 0;
         if (o.kind == EDGEDET_OP_FORK) {
-            forked = (int)o.i[0];
-            EDGEDET_REQUIRE(forked >= 1 && forked < EDGEDET_MAX_LANES, "fork: 1..3 side lanes");
             EDGEDET_CHECK_HIP(hipEventRecord(lanes->fork_ev, s));
-            for (int l = 1; l <= forked; ++l) EDGEDET_CHECK_HIP(hipStreamWaitEvent(lanes->side[l], lanes->fork_ev, 0));
+            for (int l = 1; l <= (int)o.i[0]; ++l)
+                EDGEDET_CHECK_HIP(hipStreamWaitEvent(lanes->side[l], lanes->fork_ev, 0));
         } else if (o.kind == EDGEDET_OP_JOIN) {
-            const int nl = (int)o.i[0];
-            EDGEDET_REQUIRE(nl >= 1 && nl < EDGEDET_MAX_LANES, "join: 1..3 side lanes");
-            for (int l = 1; l <= nl; ++l) {
+            for (int l = 1; l <= (int)o.i[0]; ++l) {
                 EDGEDET_CHECK_HIP(hipEventRecord(lanes->join_ev[l], lanes->side[l]));
                 EDGEDET_CHECK_HIP(hipStreamWaitEvent(s, lanes->join_ev[l], 0));
             }
-            forked = 0;
+        } else if (o.kind == EDGEDET_OP_WAIT) {
+            hipEvent_t e = lanes->wait_ev[(size_t)wait_k++];
+            EDGEDET_CHECK_HIP(hipEventRecord(e, lane_stream(o.i[1])));
+            EDGEDET_CHECK_HIP(hipStreamWaitEvent(lane_stream(o.i[0]), e, 0));
         } else {
-            const int lane = (int)o.i[EDGEDET_OP_LANE];
-            EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
-                            "op on a lane that is not forked");
-            rc = run_op(o, lane == 0 ? s : lanes->side[lane]);
+            rc = run_op(o, lane_stream(o.i[EDGEDET_OP_LANE]));
         }
         if (rc != 0) {
             set_error("op " + std::to_string(k) + " (kind " + std::to_string(o.kind) + "): " + g_error);
             return rc;
         }
     }
-    EDGEDET_REQUIRE(forked == 0, "plan ends with side lanes still forked (missing JOIN)");
     return 0;
 }
 
+// A captured plan with its own lane set (side streams + fork / join / wait events, fresh per capture):
+// the HIP runtime's captured graph keeps references to the streams and events it was captured with
+// (destroying them, by evicting a cached lane set or right after the capture, measured: a segfault in
+// the next hipGraphLaunch), so they live exactly as long as the graph, and no two graphs share one.
 struct Graph {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    std::shared_ptr<Lanes> lanes;
 };
 
 }  // namespace edgedet
@@ -500,12 +591,48 @@ extern "C" int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream) 
     return run_ops(ops, n, (hipStream_t)stream);
 }
 
+extern "C" int edgedet_plan_check(const edgedet_op* ops, int64_t n) {
+    const int64_t w = check_topology(ops, n);
+    return w < 0 ? (int)w : 0;
+}
+
+extern "C" int edgedet_release_lanes(void* stream) {
+    int dev = 0;
+    EDGEDET_CHECK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(g_lanes_mu);
+    g_lanes_by_stream.erase(std::make_pair(dev, (hipStream_t)stream));
+    return 0;
+}
+
+extern "C" int64_t edgedet_lane_sets(void) { return (int64_t)lane_cache_size(); }
+
 extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** out) {
     hipStream_t s = (hipStream_t)stream;
     EDGEDET_REQUIRE(s != nullptr, "graph capture needs a non-default stream");
+    {  // refuse a bad topology before the capture begins
+        const int64_t w = check_topology(ops, n);
+        if (w < 0) return (int)w;
+    }
     Graph* g = new Graph();
-    EDGEDET_CHECK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = run_ops(ops, n, s);
+    bool need_lanes = false;
+    for (int64_t k = 0; k < n && !need_lanes; ++k)
+        need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
+    if (need_lanes) {
+        g->lanes = make_lanes();
+        if (!g->lanes) {
+            delete g;
+            EDGEDET_REQUIRE(false, "graph_create: could not create the side lanes (streams / events)");
+        }
+    }
+    {
+        const hipError_t eb = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+        if (eb != hipSuccess) {
+            delete g;
+            set_error(std::string("hipStreamBeginCapture: ") + hipGetErrorString(eb));
+            return -2;
+        }
+    }
+    const int rc = run_ops(ops, n, s, g->lanes);
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &graph);
     if (rc != 0) {

@@ -15,6 +15,7 @@
 // and the results are bit-identical to the Python model object's (tests/test_native_model.py,
 // tests/test_gpu_native_model.py).  Everything here is host code; the kernels are in the other units.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -192,6 +193,23 @@ class Packer {
         return r;
     }
 
+    // A conv without bias and without BatchNorm (RetinaNet GroupNorm towers): a zero bias.
+    ConvW conv_nobias(const std::string& wkey, int64_t cout, int64_t cin, int k) {
+        auto key = "cn:" + wkey;
+        auto it = cache_.find(key);
+        if (it != cache_.end()) return it->second;
+        const int64_t nw = cout * cin * k * k;
+        std::vector<float> w((size_t)nw, 0.f), b((size_t)cout, 0.f);
+        if (pk_.values)
+            std::memcpy(w.data(), P_.get(wkey, nw), (size_t)nw * 4);
+        else
+            P_.check(wkey, nw);
+        ConvW r = conv_w(w, cout, cin, k, 0);
+        r.b = pk_.add(b.data(), cout);
+        cache_[key] = r;
+        return r;
+    }
+
     // pack_conv_weight on an already-built [cout][cin][k][k] fp32 weight + its bias (FC6, predictor).
     ConvW conv_given(const std::string& key, const std::vector<float>& w, const std::vector<float>& b, int64_t cout,
                      int64_t cin, int k) {
@@ -256,9 +274,12 @@ struct Ref {
     int64_t byte_off = 0;  // BUF: bytes into the buffer; W: float offset into the blob
 };
 
+// element types of workspace buffers (edgedet_buffer.dtype); Plan::buf takes the element size, or I32
+enum : int { I32 = -4 };
 struct Buf {
     std::vector<int64_t> shape;
     int esize = 4;
+    int dtype = EDGEDET_DT_F32;
     int64_t nbytes = 0;
     int64_t off = 0;
     std::string name;
@@ -267,25 +288,43 @@ struct Buf {
 struct OpRec {
     int64_t kind = 0;
     int lane = 0;
+    std::string name;
     std::map<int, int64_t> i;
     std::map<int, Ref> p;
     std::map<int, double> d;
     std::map<int, float> f;
 };
 
+struct External {
+    uint64_t weights = 0, workspace = 0, images = 0, count = 0, boxes = 0, scores = 0, labels = 0;
+    bool operator==(const External& o) const {
+        return weights == o.weights && workspace == o.workspace && images == o.images && count == o.count &&
+               boxes == o.boxes && scores == o.scores && labels == o.labels;
+    }
+};
+
 struct Plan {
+    std::shared_ptr<const std::vector<edgedet_op>> resolved;  // records of the last forward's pointers
+    External resolved_for;
     std::vector<Buf> bufs;
     std::vector<OpRec> ops;
     std::vector<std::pair<int, std::vector<uint8_t>>> consts;  // (buffer, bytes)
     int cur_lane = 0, forked = 0;
     std::map<int, int> x3;  // lane -> scratch buffer
     int64_t arena = 0;
+    uint64_t last_use = 0;
     int input = -1, out_box = -1, out_score = -1, out_label = -1, out_count = -1;
     int dets = 0;
 
     int buf(std::vector<int64_t> shape, int esize, const std::string& name) {
         Buf b;
         b.shape = shape;
+        b.dtype = esize == I32 ? EDGEDET_DT_I32
+                  : esize == 1 ? EDGEDET_DT_U8
+                  : esize == 2 ? EDGEDET_DT_I16
+                  : esize == 8 ? EDGEDET_DT_I64
+                               : EDGEDET_DT_F32;
+        if (esize == I32) esize = 4;
         b.esize = esize;
         int64_t n = 1;
         for (auto s : shape) n *= s;
@@ -345,6 +384,7 @@ struct Plan {
     void fork(int n) {
         OpRec o;
         o.kind = EDGEDET_OP_FORK;
+        o.name = "fork";
         o.i[0] = n;
         ops.push_back(o);
         forked = n;
@@ -354,6 +394,7 @@ struct Plan {
         cur_lane = 0;
         OpRec o;
         o.kind = EDGEDET_OP_JOIN;
+        o.name = "join";
         o.i[0] = forked;
         ops.push_back(o);
         forked = 0;
@@ -393,6 +434,7 @@ struct ConvArgs {
     int64_t y_pstride = -1, y_bstride = -1, y_off = 0, x_pstride = -1, x_bstride = -1;
     int res_h = -1, res_w = -1, tile = 0;
     bool in_relu = false;
+    std::string name;
 };
 
 // plan.conv_op
@@ -407,6 +449,7 @@ static void conv_op(Plan& P, const ConvArgs& a) {
     const int64_t rH = a.res_h < 0 ? Ho : a.res_h, rW = a.res_w < 0 ? Wo : a.res_w;
     OpRec o;
     o.kind = EDGEDET_OP_CONV;
+    o.name = a.name;
     const int64_t iv[25] = {B, H, W, C, Ho, Wo, a.cout, a.k, a.k, a.stride, a.pad, a.act, a.w.K, a.w.Kpad, xp, yp,
                             a.cout, a.x_bstride < 0 ? H * W * xp : a.x_bstride,
                             a.y_bstride < 0 ? Ho * Wo * yp : a.y_bstride, rH * rW * a.cout, a.y_off, rH, rW, a.tile,
@@ -431,6 +474,7 @@ static void conv_op(Plan& P, const ConvArgs& a) {
         if (a.act == 0 && a.res.kind == Ref::NONE && dense && w3) {
             OpRec m;
             m.kind = EDGEDET_OP_MEMSET;
+            m.name = a.name + ".zero";
             m.i[0] = B * Ho * Wo * a.cout * 4;
             m.p[0] = a.y;
             P.add(m);
@@ -592,6 +636,7 @@ class SSDLite {
         {
             OpRec o;
             o.kind = EDGEDET_OP_PREPROCESS;
+            o.name = "transform";
             const int64_t iv[7] = {B, H, W, S, S, S, S};
             for (int j = 0; j < 7; ++j) o.i[j] = iv[j];
             o.p[u8 ? 2 : 0] = view(inp);
@@ -621,6 +666,7 @@ class SSDLite {
             a.ys = ys;
             a.res = res;
             a.in_scale = in_scale;
+            a.name = prefix;
             conv_op(P, a);
             return Cur{P.ref(y), ys};
         };
@@ -640,6 +686,7 @@ class SSDLite {
             const int part = se_part ? P.buf({B, parts, C}, 4, prefix + ".se_partial_sums" + sfx) : -1;
             OpRec o;
             o.kind = EDGEDET_OP_DWCONV;
+            o.name = prefix;
             const int64_t iv[11] = {B, in.s[1], in.s[2], C, Ho, Wo, k, stride, pad, act, parts};
             for (int j = 0; j < 11; ++j) o.i[j] = iv[j];
             o.p[0] = in.x;
@@ -659,6 +706,7 @@ class SSDLite {
             const int hidden = P.buf({B, sq}, 4, p + ".hidden" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SE_FC;
+            o.name = p;
             const int64_t iv[5] = {B, C, sq, in.y.s[1] * in.y.s[2], in.parts};
             for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
             o.p[0] = P.ref(in.part);
@@ -681,6 +729,7 @@ class SSDLite {
             const int y = P.buf(ys, 4, pf.pp + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_MBCONV;
+            o.name = pf.pe.substr(0, pf.pe.rfind('.'));
             const int64_t iv[15] = {B, in.s[1], in.s[2], b.cin, b.exp, b.cout, Ho, Wo, b.k, b.stride, pad, b.act,
                                     w1.Kpad, w2.Kpad, (b.stride == 1 && b.cin == b.cout) ? 1 : 0};
             for (int j = 0; j < 15; ++j) o.i[j] = iv[j];
@@ -720,6 +769,7 @@ class SSDLite {
             const int y = P.buf(ys, 4, "backbone.features.0.1" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SSD_STEM;
+            o.name = "backbone.features.0.0+0.1";
             const int64_t iv[7] = {B, S, S, Ho, Wo, w0.Kpad, w1.Kpad};
             for (int j = 0; j < 7; ++j) o.i[j] = iv[j];
             o.p[0] = P.ref(x);
@@ -792,6 +842,7 @@ class SSDLite {
                 a.y_pstride = 6 * cols;
                 a.y_bstride = A * cols;
                 a.y_off = (int64_t)img0 * A * cols + off * cols;
+                a.name = p + ".1" + sfx;
                 conv_op(P, a);
             }
             off += f.s[1] * f.s[2] * 6;
@@ -812,11 +863,12 @@ class SSDLite {
             sh.ob = P.buf({Btot, DETS, 4}, 4, "out.boxes");
             sh.os = P.buf({Btot, DETS}, 4, "out.scores");
             sh.ol = P.buf({Btot, DETS}, 8, "out.labels");
-            sh.oc = P.buf({Btot}, 4, "out.count");
+            sh.oc = P.buf({Btot}, I32, "out.count");
         }
         {
             OpRec o;
             o.kind = EDGEDET_OP_SSD_SCORES;
+            o.name = "postprocess.scores" + sfx;
             o.i[0] = B;
             o.i[1] = A;
             o.i[2] = NC;
@@ -831,10 +883,11 @@ class SSDLite {
         }
         const int64_t NS = NC - 1, KM = TOPK;
         if (NS * KM <= 512 * 54 && DETS <= 1024) {
-            const int pk = P.buf({B, NS, KM}, 4, "pool.key" + sfx);
-            const int pr = P.buf({B, NS, KM}, 4, "pool.ref" + sfx);
+            const int pk = P.buf({B, NS, KM}, I32, "pool.key" + sfx);
+            const int pr = P.buf({B, NS, KM}, I32, "pool.ref" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SSD_POSTPROCESS;
+            o.name = "postprocess.nms" + sfx;
             const int64_t iv[5] = {B, A, NC, KM, DETS};
             for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
             o.p[0] = view(sh.scores_t);
@@ -851,10 +904,11 @@ class SSDLite {
             P.add(o);
         } else {
             const int rb = P.buf({B, NS, KM, 4}, 4, "rec.box" + sfx), rs = P.buf({B, NS, KM}, 4, "rec.score" + sfx);
-            const int rt = P.buf({B, NS, KM}, 4, "rec.tb" + sfx), rl = P.buf({B, NS, KM}, 4, "rec.label" + sfx);
-            const int rc = P.buf({B, NS}, 4, "rec.count" + sfx);
+            const int rt = P.buf({B, NS, KM}, I32, "rec.tb" + sfx), rl = P.buf({B, NS, KM}, I32, "rec.label" + sfx);
+            const int rc = P.buf({B, NS}, I32, "rec.count" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SSD_CLASS_NMS;
+            o.name = "postprocess.class_nms" + sfx;
             const int64_t iv[5] = {B, A, NC, TOPK, KM};
             for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
             o.p[0] = view(sh.scores_t);
@@ -869,6 +923,7 @@ class SSDLite {
             P.add(o);
             OpRec m;
             m.kind = EDGEDET_OP_MERGE_TOPK;
+            m.name = "postprocess.merge" + sfx;
             const int64_t mv[4] = {B, NS, KM, DETS};
             for (int j = 0; j < 4; ++j) m.i[j] = mv[j];
             m.p[0] = P.ref(rb);
@@ -920,43 +975,15 @@ class SSDLite {
 };
 
 // ------------------------------------------------------------------------------------ Faster R-CNN
-// anchors.rpn_anchors: per level [gh*gw*3, 4], order (y, x, a), strides = image_size // grid
-static std::vector<float> rpn_anchors(int gh, int gw, int Hp, int Wp, int size) {
-    const float ratios[3] = {0.5f, 1.0f, 2.0f};
-    float base[3][4];
-    for (int a = 0; a < 3; ++a) {
-        const float hr = std::sqrt(ratios[a]);
-        const float wr = 1.0f / hr;
-        const float ws = wr * (float)size, hs = hr * (float)size;
-        const float v[4] = {-ws / 2.0f, -hs / 2.0f, ws / 2.0f, hs / 2.0f};
-        for (int j = 0; j < 4; ++j) base[a][j] = std::nearbyint(v[j]);  // round half to even, as torch.round
-    }
-    const int sh = Hp / gh, sw = Wp / gw;
-    std::vector<float> out;
-    out.reserve((size_t)gh * gw * 12);
-    for (int y = 0; y < gh; ++y)
-        for (int x = 0; x < gw; ++x)
-            for (int a = 0; a < 3; ++a) {
-                const float fx = (float)((int64_t)x * sw), fy = (float)((int64_t)y * sh);
-                out.push_back(fx + base[a][0]);
-                out.push_back(fy + base[a][1]);
-                out.push_back(fx + base[a][2]);
-                out.push_back(fy + base[a][3]);
-            }
-    return out;
-}
-
-class FasterRCNN {
+// Shared by Faster R-CNN and RetinaNet (models.FasterRCNNFPNv2._lower_body): GeneralizedRCNNTransform
+// (min 800 / max 1333, ImageNet mean / std, pad to /32) and the ResNet-50 body C2..C5.
+class ResNetFPN {
   public:
     static constexpr double EPS = 1e-5;
     static constexpr int MIN_SIZE = 800, MAX_SIZE = 1333, DIV = 32;
-    static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
-    static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
-                            BOX_MIN = 1e-2;
 
-    FasterRCNN(const Config& c, Packer& pk) : cfg_(c), pk_(pk) {}
-
-    void pack_all() { lower(1, MIN_SIZE, MIN_SIZE, false, true); }
+    ResNetFPN(const Config& c, Packer& pk) : cfg_(c), pk_(pk) {}
+    virtual ~ResNetFPN() = default;
 
     // [TV] GeneralizedRCNNTransform resize (detect.py:78): the scale is a float32 tensor
     // op, min(800. / min_f32, 1333. / max_f32), where `float / Tensor` is reciprocal(t) * x; the sizes
@@ -969,21 +996,112 @@ class FasterRCNN {
         Wo = (int)std::floor(W * scale);
     }
 
-    std::unique_ptr<Plan> lower(int B, int H, int W, bool u8, bool pack_only = false) {
-        auto Pp = std::make_unique<Plan>();
-        Plan& P = *Pp;
-        const int NC = cfg_.num_classes;
-        int Ho, Wo;
-        resized_size(H, W, Ho, Wo);
-        const int Hp = (Ho + DIV - 1) / DIV * DIV, Wp = (Wo + DIV - 1) / DIV * DIV;
-        const int inp = P.buf({B, 3, H, W}, u8 ? 1 : 4, "images");
-        const int x = P.buf({B, Hp, Wp, 4}, 4, "pre");
+  protected:
+    // options of one conv (models.FasterRCNNFPNv2._lower_body.conv): BatchNorm prefix, or a bias key,
+    // or neither (no bias: RetinaNet GroupNorm towers); fused input transform; strided output
+    struct COpt {
+        std::string bnp, bias_key, name;
+        Ref res, in_scale, in_shift;
+        int res_h = -1, res_w = -1;
+        int64_t cin_pad = 0;
+        bool in_relu = false;
+        int out = -1;  // store into this buffer (pixel stride out_p, batch stride out_b, element offset out_off)
+        int64_t out_p = -1, out_b = -1, out_off = 0;
+    };
+
+    Cur conv(Plan& P, const Cur& in, const std::string& wkey, int64_t cout, int k, int stride, int act,
+             const COpt& o) {
+        ConvW w;
+        if (!o.bias_key.empty())
+            w = pk_.conv_bias(wkey, o.bias_key, cout, in.s[3], k);
+        else if (o.bnp.empty())
+            w = pk_.conv_nobias(wkey, cout, in.s[3], k);
+        else
+            w = pk_.conv_bn(wkey, o.bnp, EPS, cout, o.cin_pad ? 3 : in.s[3], k, false, o.cin_pad);
+        const int pad = (k - 1) / 2;
+        const int64_t Ho_ = (in.s[1] + 2 * pad - k) / stride + 1, Wo_ = (in.s[2] + 2 * pad - k) / stride + 1;
+        std::vector<int64_t> ys = {in.s[0], Ho_, Wo_, cout};
+        const int y = o.out >= 0 ? o.out : P.buf(ys, 4, o.name.empty() ? wkey : o.name);
+        ConvArgs a;
+        a.x = in.x;
+        a.xs = in.s;
+        a.w = w;
+        a.cout = cout;
+        a.k = k;
+        a.stride = stride;
+        a.pad = pad;
+        a.act = act;
+        a.y = P.ref(y);
+        a.ys = ys;
+        a.res = o.res;
+        a.res_h = o.res_h;
+        a.res_w = o.res_w;
+        a.in_relu = o.in_relu;
+        a.in_scale = o.in_scale;
+        a.in_shift = o.in_shift;
+        a.name = o.name.empty() ? wkey : o.name;
+        if (o.out >= 0) {
+            a.y_pstride = o.out_p;
+            a.y_bstride = o.out_b;
+            a.y_off = o.out_off;
+        }
+        conv_op(P, a);
+        return Cur{P.ref(y), ys};
+    }
+    Cur conv_bn(Plan& P, const Cur& in, const std::string& wkey, const std::string& bnp, int64_t cout, int k,
+                int stride, int act, Ref res = Ref(), int res_h = -1, int res_w = -1, bool in_relu = false) {
+        COpt o;
+        o.bnp = bnp;
+        o.res = res;
+        o.res_h = res_h;
+        o.res_w = res_w;
+        o.in_relu = in_relu;
+        return conv(P, in, wkey, cout, k, stride, act, o);
+    }
+    Cur conv_b(Plan& P, const Cur& in, const std::string& p, int64_t cout, int k, int stride, int act,
+               const std::string& name = "", Ref res = Ref(), int res_h = -1, int res_w = -1, bool in_relu = false) {
+        COpt o;
+        o.bias_key = p + ".bias";
+        o.name = name;
+        o.res = res;
+        o.res_h = res_h;
+        o.res_w = res_w;
+        o.in_relu = in_relu;
+        return conv(P, in, p + ".weight", cout, k, stride, act, o);
+    }
+    Cur maxpool(Plan& P, const Cur& in, int k, int stride, int pad, const std::string& name) {
+        const int64_t Ho_ = (in.s[1] + 2 * pad - k) / stride + 1, Wo_ = (in.s[2] + 2 * pad - k) / stride + 1;
+        std::vector<int64_t> ys = {in.s[0], Ho_, Wo_, in.s[3]};
+        const int y = P.buf(ys, 4, name);
+        OpRec o;
+        o.kind = EDGEDET_OP_MAXPOOL;
+        o.name = name;
+        const int64_t iv[9] = {in.s[0], in.s[1], in.s[2], in.s[3], Ho_, Wo_, k, stride, pad};
+        for (int j = 0; j < 9; ++j) o.i[j] = iv[j];
+        o.p[0] = in.x;
+        o.p[1] = P.ref(y);
+        P.add(o);
+        return Cur{P.ref(y), ys};
+    }
+
+    struct Body {
+        int inp = -1, Ho = 0, Wo = 0, Hp = 0, Wp = 0;
+        std::vector<Cur> cs;  // C2..C5
+    };
+    Body body(Plan& P, int B, int H, int W, bool u8) {
+        Body r;
+        resized_size(H, W, r.Ho, r.Wo);
+        r.Hp = (r.Ho + DIV - 1) / DIV * DIV;
+        r.Wp = (r.Wo + DIV - 1) / DIV * DIV;
+        r.inp = P.buf({B, 3, H, W}, u8 ? 1 : 4, "images");
+        const int x = P.buf({B, r.Hp, r.Wp, 4}, 4, "pre");
         {
             OpRec o;
             o.kind = EDGEDET_OP_PREPROCESS;
-            const int64_t iv[7] = {B, H, W, Ho, Wo, Hp, Wp};
+            o.name = "transform";
+            const int64_t iv[7] = {B, H, W, r.Ho, r.Wo, r.Hp, r.Wp};
             for (int j = 0; j < 7; ++j) o.i[j] = iv[j];
-            o.p[u8 ? 2 : 0] = P.ref(inp);
+            o.p[u8 ? 2 : 0] = P.ref(r.inp);
             o.p[1] = P.ref(x);
             const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
             for (int j = 0; j < 3; ++j) {
@@ -992,85 +1110,103 @@ class FasterRCNN {
             }
             P.add(o);
         }
-        Cur cur{P.ref(x), {B, Hp, Wp, 4}};
-
-        // conv helper (models.FasterRCNNFPNv2._lower_body.conv)
-        auto conv = [&](const Cur& in, const std::string& wkey, const std::string& bnp, int64_t cout, int k,
-                        int stride, int act, Ref res = Ref(), int res_h = -1, int res_w = -1, int64_t cin_pad = 0,
-                        const std::string& bias_key = "", const std::string& name = "", bool in_relu = false) {
-            ConvW w = bias_key.empty() ? pk_.conv_bn(wkey, bnp, EPS, cout, cin_pad ? 3 : in.s[3], k, false, cin_pad)
-                                       : pk_.conv_bias(wkey, bias_key, cout, in.s[3], k);
-            const int pad = (k - 1) / 2;
-            const int64_t Ho_ = (in.s[1] + 2 * pad - k) / stride + 1, Wo_ = (in.s[2] + 2 * pad - k) / stride + 1;
-            std::vector<int64_t> ys = {in.s[0], Ho_, Wo_, cout};
-            const int y = P.buf(ys, 4, name.empty() ? wkey : name);
-            ConvArgs a;
-            a.x = in.x;
-            a.xs = in.s;
-            a.w = w;
-            a.cout = cout;
-            a.k = k;
-            a.stride = stride;
-            a.pad = pad;
-            a.act = act;
-            a.y = P.ref(y);
-            a.ys = ys;
-            a.res = res;
-            a.res_h = res_h;
-            a.res_w = res_w;
-            a.in_relu = in_relu;
-            conv_op(P, a);
-            return Cur{P.ref(y), ys};
-        };
-        auto maxpool = [&](const Cur& in, int k, int stride, int pad, const std::string& name) {
-            const int64_t Ho_ = (in.s[1] + 2 * pad - k) / stride + 1, Wo_ = (in.s[2] + 2 * pad - k) / stride + 1;
-            std::vector<int64_t> ys = {in.s[0], Ho_, Wo_, in.s[3]};
-            const int y = P.buf(ys, 4, name);
-            OpRec o;
-            o.kind = EDGEDET_OP_MAXPOOL;
-            const int64_t iv[9] = {in.s[0], in.s[1], in.s[2], in.s[3], Ho_, Wo_, k, stride, pad};
-            for (int j = 0; j < 9; ++j) o.i[j] = iv[j];
-            o.p[0] = in.x;
-            o.p[1] = P.ref(y);
-            P.add(o);
-            return Cur{P.ref(y), ys};
-        };
-
-        // ---- ResNet-50 body
+        Cur cur{P.ref(x), {B, r.Hp, r.Wp, 4}};
         const std::string pb = "backbone.body.";
-        cur = conv(cur, pb + "conv1.weight", pb + "bn1", 64, 7, 2, A_RE, Ref(), -1, -1, 4);
-        cur = maxpool(cur, 3, 2, 1, "backbone.body.maxpool");
+        {
+            COpt o;
+            o.bnp = pb + "bn1";
+            o.cin_pad = 4;
+            cur = conv(P, cur, pb + "conv1.weight", 64, 7, 2, A_RE, o);
+        }
+        cur = maxpool(P, cur, 3, 2, 1, "backbone.body.maxpool");
+        // deep-K 3x3 convs on small maps fill the GPU only with split-K (tile 26), which cannot apply the
+        // ReLU: conv3 then applies it to its input
         const bool splitk_defer = env_int("EDGEDET_SPLITK_DEFER", 1) == 1;
         const char* lname[4] = {"layer1", "layer2", "layer3", "layer4"};
         const int nblk[4] = {3, 4, 6, 3}, width[4] = {64, 128, 256, 512}, lstride[4] = {1, 2, 2, 2};
-        std::vector<Cur> cs;
         for (int L = 0; L < 4; ++L) {
             for (int bi = 0; bi < nblk[L]; ++bi) {
                 const std::string q = pb + lname[L] + "." + std::to_string(bi) + ".";
                 const int s = bi == 0 ? lstride[L] : 1;
                 const int wd = width[L];
-                Cur y = conv(cur, q + "conv1.weight", q + "bn1", wd, 1, 1, A_RE);
+                Cur y = conv_bn(P, cur, q + "conv1.weight", q + "bn1", wd, 1, 1, A_RE);
                 const int64_t m = y.s[0] * ((y.s[1] - 1) / s + 1) * ((y.s[2] - 1) / s + 1);
                 const bool defer = splitk_defer && 9 * wd >= 2048 && ((m + 255) / 256) * ((wd + 127) / 128) < 200;
-                y = conv(y, q + "conv2.weight", q + "bn2", wd, 3, s, defer ? A_NONE : A_RE);
-                Cur idn = bi == 0 ? conv(cur, q + "downsample.0.weight", q + "downsample.1", wd * 4, 1, s, A_NONE) : cur;
-                cur = conv(y, q + "conv3.weight", q + "bn3", wd * 4, 1, 1, A_RE, idn.x, -1, -1, 0, "", "", defer);
+                y = conv_bn(P, y, q + "conv2.weight", q + "bn2", wd, 3, s, defer ? A_NONE : A_RE);
+                Cur idn = bi == 0 ? conv_bn(P, cur, q + "downsample.0.weight", q + "downsample.1", wd * 4, 1, s, A_NONE)
+                                  : cur;
+                cur = conv_bn(P, y, q + "conv3.weight", q + "bn3", wd * 4, 1, 1, A_RE, idn.x, -1, -1, defer);
             }
-            cs.push_back(cur);
+            r.cs.push_back(cur);
         }
+        return r;
+    }
+
+    Config cfg_;
+    Packer& pk_;
+};
+
+// anchors.rpn_anchors / retina_anchors: per level [gh*gw*A, 4], order (y, x, a), a ratio-major over the
+// level's scales; strides = image_size // grid
+static std::vector<float> grid_anchors(int gh, int gw, int Hp, int Wp, const std::vector<int>& scales) {
+    const float ratios[3] = {0.5f, 1.0f, 2.0f};
+    std::vector<std::array<float, 4>> base;
+    for (int a = 0; a < 3; ++a) {
+        const float hr = std::sqrt(ratios[a]);
+        const float wr = 1.0f / hr;
+        for (int sc : scales) {
+            const float ws = wr * (float)sc, hs = hr * (float)sc;
+            const float v[4] = {-ws / 2.0f, -hs / 2.0f, ws / 2.0f, hs / 2.0f};
+            std::array<float, 4> b;
+            for (int j = 0; j < 4; ++j) b[(size_t)j] = std::nearbyint(v[j]);  // round half to even, as torch.round
+            base.push_back(b);
+        }
+    }
+    const int sh = Hp / gh, sw = Wp / gw;
+    std::vector<float> out;
+    out.reserve((size_t)gh * gw * base.size() * 4);
+    for (int y = 0; y < gh; ++y)
+        for (int x = 0; x < gw; ++x)
+            for (auto& b : base) {
+                const float fx = (float)((int64_t)x * sw), fy = (float)((int64_t)y * sh);
+                out.push_back(fx + b[0]);
+                out.push_back(fy + b[1]);
+                out.push_back(fx + b[2]);
+                out.push_back(fy + b[3]);
+            }
+    return out;
+}
+
+class FasterRCNN : public ResNetFPN {
+  public:
+    static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
+    static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
+                            BOX_MIN = 1e-2;
+
+    FasterRCNN(const Config& c, Packer& pk) : ResNetFPN(c, pk) {}
+
+    void pack_all() { lower(1, MIN_SIZE, MIN_SIZE, false, true); }
+
+    std::unique_ptr<Plan> lower(int B, int H, int W, bool u8, bool pack_only = false) {
+        auto Pp = std::make_unique<Plan>();
+        Plan& P = *Pp;
+        const int NC = cfg_.num_classes;
+        Body bd = body(P, B, H, W, u8);
+        const int Ho = bd.Ho, Wo = bd.Wo, Hp = bd.Hp, Wp = bd.Wp;
+        const std::vector<Cur>& cs = bd.cs;
 
         // ---- FPN + LastLevelMaxPool
         const std::string f = "backbone.fpn.";
-        Cur last = conv(cs[3], f + "inner_blocks.3.0.weight", f + "inner_blocks.3.1", 256, 1, 1, A_NONE);
-        std::vector<Cur> outs = {conv(last, f + "layer_blocks.3.0.weight", f + "layer_blocks.3.1", 256, 3, 1, A_NONE)};
+        Cur last = conv_bn(P, cs[3], f + "inner_blocks.3.0.weight", f + "inner_blocks.3.1", 256, 1, 1, A_NONE);
+        std::vector<Cur> outs = {conv_bn(P, last, f + "layer_blocks.3.0.weight", f + "layer_blocks.3.1", 256, 3, 1, A_NONE)};
         for (int i : {2, 1, 0}) {
             const std::string si = std::to_string(i);
-            last = conv(cs[(size_t)i], f + "inner_blocks." + si + ".0.weight", f + "inner_blocks." + si + ".1", 256, 1,
-                        1, A_NONE, last.x, (int)last.s[1], (int)last.s[2]);
-            outs.insert(outs.begin(),
-                        conv(last, f + "layer_blocks." + si + ".0.weight", f + "layer_blocks." + si + ".1", 256, 3, 1, A_NONE));
+            last = conv_bn(P, cs[(size_t)i], f + "inner_blocks." + si + ".0.weight", f + "inner_blocks." + si + ".1", 256,
+                           1, 1, A_NONE, last.x, (int)last.s[1], (int)last.s[2]);
+            outs.insert(outs.begin(), conv_bn(P, last, f + "layer_blocks." + si + ".0.weight",
+                                              f + "layer_blocks." + si + ".1", 256, 3, 1, A_NONE));
         }
-        outs.push_back(maxpool(outs.back(), 1, 2, 0, "backbone.fpn.extra_blocks.pool"));
+        outs.push_back(maxpool(P, outs.back(), 1, 2, 0, "backbone.fpn.extra_blocks.pool"));
         if (pack_only) {
             for (const char* k : {"rpn.head.conv.0.0", "rpn.head.conv.1.0"})
                 pk_.conv_bias(std::string(k) + ".weight", std::string(k) + ".bias", 256, 256, 3);
@@ -1093,14 +1229,10 @@ class FasterRCNN {
         for (size_t lvl = 0; lvl < outs.size(); ++lvl) {
             P.lane((int)(lvl % 4));
             const std::string at = "@" + std::to_string(lvl);
-            Cur t = conv(outs[lvl], "rpn.head.conv.0.0.weight", "", 256, 3, 1, A_RE, Ref(), -1, -1, 0,
-                         "rpn.head.conv.0.0.bias", "rpn.head.conv.0" + at);
-            t = conv(t, "rpn.head.conv.1.0.weight", "", 256, 3, 1, A_RE, Ref(), -1, -1, 0, "rpn.head.conv.1.0.bias",
-                     "rpn.head.conv.1" + at);
-            Cur o = conv(t, "rpn.head.cls_logits.weight", "", 3, 1, 1, A_NONE, Ref(), -1, -1, 0,
-                         "rpn.head.cls_logits.bias", "rpn.head.cls_logits" + at);
-            Cur d = conv(t, "rpn.head.bbox_pred.weight", "", 12, 1, 1, A_NONE, Ref(), -1, -1, 0,
-                         "rpn.head.bbox_pred.bias", "rpn.head.bbox_pred" + at);
+            Cur t = conv_b(P, outs[lvl], "rpn.head.conv.0.0", 256, 3, 1, A_RE, "rpn.head.conv.0" + at);
+            t = conv_b(P, t, "rpn.head.conv.1.0", 256, 3, 1, A_RE, "rpn.head.conv.1" + at);
+            Cur o = conv_b(P, t, "rpn.head.cls_logits", 3, 1, 1, A_NONE, "rpn.head.cls_logits" + at);
+            Cur d = conv_b(P, t, "rpn.head.bbox_pred", 12, 1, 1, A_NONE, "rpn.head.bbox_pred" + at);
             heads.push_back({o.x, d.x});
             grids.push_back({(int)outs[lvl].s[1], (int)outs[lvl].s[2]});
         }
@@ -1108,17 +1240,18 @@ class FasterRCNN {
         std::vector<int> anchor_bufs;
         const int sizes[5] = {32, 64, 128, 256, 512};
         for (size_t l = 0; l < grids.size(); ++l) {
-            auto a = rpn_anchors(grids[l].first, grids[l].second, Hp, Wp, sizes[l]);
+            auto a = grid_anchors(grids[l].first, grids[l].second, Hp, Wp, {sizes[l]});
             anchor_bufs.push_back(P.cnst(a, {(int64_t)a.size() / 4, 4}, "rpn.anchors@" + std::to_string(l)));
         }
         const int L = (int)outs.size();
         const int KM = RPN_PRE;
         const int rb = P.buf({B, L, KM, 4}, 4, "rpn.rec.box"), rs = P.buf({B, L, KM}, 4, "rpn.rec.score");
-        const int rt = P.buf({B, L, KM}, 4, "rpn.rec.tb"), rl = P.buf({B, L, KM}, 4, "rpn.rec.lvl");
-        const int rc = P.buf({B, L}, 4, "rpn.rec.count");
+        const int rt = P.buf({B, L, KM}, I32, "rpn.rec.tb"), rl = P.buf({B, L, KM}, I32, "rpn.rec.lvl");
+        const int rc = P.buf({B, L}, I32, "rpn.rec.count");
         {
             OpRec o;
             o.kind = EDGEDET_OP_RPN_LEVEL_NMS;
+            o.name = "rpn.filter_proposals";
             const int64_t iv[6] = {B, L, 0, Aa, RPN_PRE, KM};
             for (int j = 0; j < 6; ++j) o.i[j] = iv[j];
             for (int l = 0; l < L; ++l) {
@@ -1138,10 +1271,11 @@ class FasterRCNN {
         }
         const int R = RPN_POST;
         const int props = P.buf({B, R, 4}, 4, "proposals"), pscore = P.buf({B, R}, 4, "proposal_scores");
-        const int pcount = P.buf({B}, 4, "proposal_count");
+        const int pcount = P.buf({B}, I32, "proposal_count");
         {
             OpRec o;
             o.kind = EDGEDET_OP_MERGE_TOPK;
+            o.name = "rpn.post_nms_top_n";
             const int64_t iv[4] = {B, L, KM, R};
             for (int j = 0; j < 4; ++j) o.i[j] = iv[j];
             const int recs[5] = {rb, rs, rt, rl, rc};
@@ -1160,6 +1294,7 @@ class FasterRCNN {
         {
             OpRec o;
             o.kind = EDGEDET_OP_ROI_ALIGN;
+            o.name = "roi_heads.box_roi_pool";
             const int64_t iv[11] = {1, (int64_t)B * R, R, B, C, 7, 7, 2, 4, 2, 5};
             for (int j = 0; j < 11; ++j) o.i[j] = iv[j];
             o.p[4] = P.ref(props);
@@ -1181,7 +1316,7 @@ class FasterRCNN {
         Cur bc{P.ref(roi), {(int64_t)B * R, 7, 7, C}};
         for (int i = 0; i < 4; ++i) {
             const std::string p = "roi_heads.box_head." + std::to_string(i);
-            bc = conv(bc, p + ".0.weight", p + ".1", 256, 3, 1, A_RE);
+            bc = conv_bn(P, bc, p + ".0.weight", p + ".1", 256, 3, 1, A_RE);
         }
         {
             ConvW w = fc6();
@@ -1194,6 +1329,7 @@ class FasterRCNN {
             a.act = A_RE;
             a.y = P.ref(fc);
             a.ys = {(int64_t)B * R, 1, 1, 1024};
+            a.name = "roi_heads.box_head.5";
             conv_op(P, a);
             ConvW wp = predictor();
             const int LD = 456;
@@ -1207,6 +1343,7 @@ class FasterRCNN {
             b.ys = {(int64_t)B * R, 1, 1, 5 * NC};
             b.y_pstride = LD;
             b.y_bstride = LD;
+            b.name = "roi_heads.box_predictor";
             conv_op(P, b);
 
             // ---- RoIHeads.postprocess_detections
@@ -1214,6 +1351,7 @@ class FasterRCNN {
             const int bxs = P.buf({B, R, NC, 4}, 4, "box_decoded");
             OpRec o;
             o.kind = EDGEDET_OP_BOX_SCORES;
+            o.name = "roi_heads.scores_decode";
             const int64_t iv[6] = {LD, B, R, NC, 4 * NC, 0};
             for (int j = 0; j < 6; ++j) o.i[j] = iv[j];
             o.p[0] = P.ref(pred);
@@ -1226,10 +1364,11 @@ class FasterRCNN {
             P.add(o);
             const int NS = NC - 1;
             const int b0 = P.buf({B, NS, R, 4}, 4, "box.rec.box"), b1 = P.buf({B, NS, R}, 4, "box.rec.score");
-            const int b2 = P.buf({B, NS, R}, 4, "box.rec.tb"), b3 = P.buf({B, NS, R}, 4, "box.rec.lbl");
-            const int b4 = P.buf({B, NS}, 4, "box.rec.count");
+            const int b2 = P.buf({B, NS, R}, I32, "box.rec.tb"), b3 = P.buf({B, NS, R}, I32, "box.rec.lbl");
+            const int b4 = P.buf({B, NS}, I32, "box.rec.count");
             OpRec n;
             n.kind = EDGEDET_OP_BOX_CLASS_NMS;
+            n.name = "roi_heads.class_nms";
             const int64_t nv[4] = {B, R, NC, R};
             for (int j = 0; j < 4; ++j) n.i[j] = nv[j];
             n.p[0] = P.ref(scores);
@@ -1251,9 +1390,10 @@ class FasterRCNN {
             P.out_box = P.buf({B, N, 4}, 4, "out.boxes");
             P.out_score = P.buf({B, N}, 4, "out.scores");
             P.out_label = P.buf({B, N}, 8, "out.labels");
-            P.out_count = P.buf({B}, 4, "out.count");
+            P.out_count = P.buf({B}, I32, "out.count");
             OpRec m;
             m.kind = EDGEDET_OP_MERGE_TOPK;
+            m.name = "roi_heads.detections_per_img";
             const int64_t mv[4] = {B, NS, R, N};
             for (int j = 0; j < 4; ++j) m.i[j] = mv[j];
             for (int j = 0; j < 5; ++j) m.p[j] = P.ref(brec[j]);
@@ -1264,7 +1404,7 @@ class FasterRCNN {
             m.p[9] = P.ref(P.out_count);
             P.add(m);
         }
-        P.input = inp;
+        P.input = bd.inp;
         P.dets = BOX_DETS;
         return Pp;
     }
@@ -1305,8 +1445,229 @@ class FasterRCNN {
         return pk_.conv_given("pred", w, b, 5 * NC, 1024, 1);
     }
 
-    Config cfg_;
-    Packer& pk_;
+};
+
+
+// retinanet_resnet50_fpn_v2 (detect.py:34-38; models.RetinaNetFPNv2): the ResNet-50 body, FPN over
+// C3..C5 (convs with bias, no norm) + LastLevelP6P7 (P6 on C5, P7 on relu(P6): the ReLU applied as P7's
+// conv loads its input), GroupNorm(32) head towers whose normalised tensors are never written
+// (GN_STATS -> per (image, channel) scale / shift applied, with the ReLU, by the next conv's A load),
+// cls / box convs storing straight into the concatenated [B, sum(HWA), K] / [B, sum(HWA), 4] tensors.
+class RetinaNet : public ResNetFPN {
+  public:
+    static constexpr int DETS = 300, TOPK = 1000, GROUPS = 32, A = 9;
+    static constexpr double SCORE = 0.05, NMS = 0.5, GN_EPS = 1e-5;
+    static constexpr int64_t SELECT_CHUNK = 1 << 16;
+
+    RetinaNet(const Config& c, Packer& pk) : ResNetFPN(c, pk) {}
+
+    void pack_all() { lower(1, MIN_SIZE, MIN_SIZE, false, true); }
+
+    std::unique_ptr<Plan> lower(int B, int H, int W, bool u8, bool pack_only = false) {
+        auto Pp = std::make_unique<Plan>();
+        Plan& P = *Pp;
+        const int K = cfg_.num_classes;
+        Body bd = body(P, B, H, W, u8);
+        const int Ho = bd.Ho, Wo = bd.Wo, Hp = bd.Hp, Wp = bd.Wp;
+        const std::string f = "backbone.fpn.";
+        const Cur &c3 = bd.cs[1], &c4 = bd.cs[2], &c5 = bd.cs[3];
+        Cur last = conv_b(P, c5, f + "inner_blocks.2.0", 256, 1, 1, A_NONE, f + "inner_blocks.2.0.weight");
+        std::vector<Cur> outs = {conv_b(P, last, f + "layer_blocks.2.0", 256, 3, 1, A_NONE, f + "layer_blocks.2.0.weight")};
+        const std::pair<int, const Cur*> lat[2] = {{1, &c4}, {0, &c3}};
+        for (auto& ic : lat) {
+            const std::string si = std::to_string(ic.first);
+            last = conv_b(P, *ic.second, f + "inner_blocks." + si + ".0", 256, 1, 1, A_NONE,
+                          f + "inner_blocks." + si + ".0.weight", last.x, (int)last.s[1], (int)last.s[2]);
+            outs.insert(outs.begin(), conv_b(P, last, f + "layer_blocks." + si + ".0", 256, 3, 1, A_NONE,
+                                             f + "layer_blocks." + si + ".0.weight"));
+        }
+        Cur p6 = conv_b(P, c5, f + "extra_blocks.p6", 256, 3, 2, A_NONE, f + "extra_blocks.p6.weight");
+        Cur p7 = conv_b(P, p6, f + "extra_blocks.p7", 256, 3, 2, A_NONE, f + "extra_blocks.p7.weight", Ref(), -1, -1,
+                        true);
+        outs.push_back(p6);
+        outs.push_back(p7);
+        const char* br_name[2] = {"classification_head", "regression_head"};
+        const char* last_name[2] = {"cls_logits", "bbox_reg"};
+        const int kk_of[2] = {K, 4};
+        if (pack_only) {
+            for (int h = 0; h < 2; ++h) {
+                for (int i = 0; i < 4; ++i) {
+                    const std::string q = std::string("head.") + br_name[h] + ".conv." + std::to_string(i);
+                    pk_.conv_nobias(q + ".0.weight", 256, 256, 3);
+                    gn(q + ".1");
+                }
+                const std::string lp = std::string("head.") + br_name[h] + "." + last_name[h];
+                pk_.conv_bias(lp + ".weight", lp + ".bias", (int64_t)A * kk_of[h], 256, 3);
+            }
+            return Pp;
+        }
+
+        std::vector<std::pair<int, int>> grids;
+        std::vector<int64_t> na, a0;
+        int64_t Atot = 0;
+        for (auto& o : outs) {
+            grids.push_back({(int)o.s[1], (int)o.s[2]});
+            na.push_back(o.s[1] * o.s[2] * A);
+            a0.push_back(Atot);
+            Atot += o.s[1] * o.s[2] * A;
+        }
+        const int cls = P.buf({B, Atot, K}, 4, "head.cls_logits");
+        const int reg = P.buf({B, Atot, 4}, 4, "head.bbox_regression");
+        const int64_t C = 256;
+        P.fork(3);  // the five levels' head towers are independent
+        for (size_t lvl = 0; lvl < outs.size(); ++lvl) {
+            P.lane((int)(lvl % 4));
+            const int64_t hw = outs[lvl].s[1] * outs[lvl].s[2];
+            const std::string at = "@" + std::to_string(lvl);
+            for (int h = 0; h < 2; ++h) {
+                const int kk = kk_of[h];
+                const int dst = kk == K ? cls : reg;
+                Cur t = outs[lvl];
+                Ref sc, sh;
+                for (int i = 0; i < 4; ++i) {
+                    const std::string q = std::string("head.") + br_name[h] + ".conv." + std::to_string(i) + ".";
+                    COpt o;
+                    o.in_scale = sc;
+                    o.in_shift = sh;
+                    o.in_relu = i > 0;
+                    o.name = q + "0" + at;
+                    t = conv(P, t, q + "0.weight", C, 3, 1, A_NONE, o);
+                    WRef g, b;
+                    gn(q + "1", &g, &b);
+                    const int scb = P.buf({B, C}, 4, q + "1.scale" + at), shb = P.buf({B, C}, 4, q + "1.shift" + at);
+                    OpRec s;
+                    s.kind = EDGEDET_OP_GN_STATS;
+                    s.name = q + "1" + at;
+                    s.i[0] = B;
+                    s.i[1] = hw;
+                    s.i[2] = C;
+                    s.i[3] = GROUPS;
+                    s.p[0] = t.x;
+                    s.p[1] = Plan::wref(g);
+                    s.p[2] = Plan::wref(b);
+                    s.p[3] = P.ref(scb);
+                    s.p[4] = P.ref(shb);
+                    s.f[0] = (float)GN_EPS;
+                    P.add(s);
+                    sc = P.ref(scb);
+                    sh = P.ref(shb);
+                }
+                const std::string lp = std::string("head.") + br_name[h] + "." + last_name[h];
+                COpt o;
+                o.bias_key = lp + ".bias";
+                o.in_scale = sc;
+                o.in_shift = sh;
+                o.in_relu = true;
+                o.out = dst;
+                o.out_p = (int64_t)A * kk;
+                o.out_b = Atot * kk;
+                o.out_off = a0[lvl] * kk;
+                o.name = lp + at;
+                conv(P, t, lp + ".weight", (int64_t)A * kk, 3, 1, A_NONE, o);
+            }
+        }
+        P.join();
+        std::vector<float> anchors;
+        for (size_t l = 0; l < grids.size(); ++l) {
+            const int x = 32 << l;
+            const std::vector<int> scales = {x, (int)(x * std::pow(2.0, 1.0 / 3)), (int)(x * std::pow(2.0, 2.0 / 3))};
+            auto a = grid_anchors(grids[l].first, grids[l].second, Hp, Wp, scales);
+            anchors.insert(anchors.end(), a.begin(), a.end());
+        }
+        const int anc = P.cnst(anchors, {Atot, 4}, "anchors");
+
+        // ---- RetinaNet.postprocess_detections
+        const int L = (int)outs.size(), KM = TOPK;
+        const int lrec[5] = {P.buf({B, L, KM, 4}, 4, "retina.cand.box"), P.buf({B, L, KM}, 4, "retina.cand.score"),
+                             P.buf({B, L, KM}, I32, "retina.cand.tb"), P.buf({B, L, KM}, I32, "retina.cand.label"),
+                             P.buf({B, L}, I32, "retina.cand.count")};
+        int64_t nchunk = 0;
+        for (int64_t n : na) nchunk = std::max<int64_t>(nchunk, (n * K + SELECT_CHUNK - 1) / SELECT_CHUNK);
+        const int ck = P.buf({B, L, nchunk, 1024}, I32, "retina.chunk.key");
+        const int ci = P.buf({B, L, nchunk, 1024}, I32, "retina.chunk.idx");
+        const int cc = P.buf({B, L, nchunk}, I32, "retina.chunk.count");
+        {
+            OpRec o;
+            o.kind = EDGEDET_OP_RETINA_SELECT;
+            o.name = "retina.select_topk";
+            const int64_t iv[6] = {B, L, Atot, K, TOPK, KM};
+            for (int j = 0; j < 6; ++j) o.i[j] = iv[j];
+            o.i[16] = SELECT_CHUNK;
+            o.i[17] = nchunk;
+            for (int l = 0; l < L; ++l) {
+                o.i[6 + l] = a0[(size_t)l];
+                o.i[11 + l] = na[(size_t)l];
+            }
+            o.p[0] = P.ref(cls);
+            o.p[1] = P.ref(reg);
+            o.p[2] = P.ref(anc);
+            for (int j = 0; j < 5; ++j) o.p[3 + j] = P.ref(lrec[j]);
+            o.p[8] = P.ref(ck);
+            o.p[9] = P.ref(ci);
+            o.p[10] = P.ref(cc);
+            o.f[0] = (float)Ho;
+            o.f[1] = (float)Wo;
+            o.f[2] = (float)SCORE;
+            P.add(o);
+        }
+        const int N = DETS;
+        const int crec[5] = {P.buf({B, K, N, 4}, 4, "retina.kept.box"), P.buf({B, K, N}, 4, "retina.kept.score"),
+                             P.buf({B, K, N}, I32, "retina.kept.tb"), P.buf({B, K, N}, I32, "retina.kept.lbl"),
+                             P.buf({B, K}, I32, "retina.kept.count")};
+        {
+            OpRec o;
+            o.kind = EDGEDET_OP_RETINA_CLASS_NMS;
+            o.name = "retina.batched_nms";
+            const int64_t iv[5] = {B, L, KM, K, N};
+            for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
+            for (int j = 0; j < 5; ++j) {
+                o.p[j] = P.ref(lrec[j]);
+                o.p[5 + j] = P.ref(crec[j]);
+            }
+            o.d[0] = NMS;
+            P.add(o);
+        }
+        std::vector<float> ratio;
+        for (int b = 0; b < B; ++b) {
+            ratio.push_back((float)W / (float)Wo);
+            ratio.push_back((float)H / (float)Ho);
+        }
+        const int rbuf = P.cnst(ratio, {B, 2}, "ratio");
+        P.out_box = P.buf({B, N, 4}, 4, "out.boxes");
+        P.out_score = P.buf({B, N}, 4, "out.scores");
+        P.out_label = P.buf({B, N}, 8, "out.labels");
+        P.out_count = P.buf({B}, I32, "out.count");
+        {
+            OpRec m;
+            m.kind = EDGEDET_OP_MERGE_TOPK;
+            m.name = "retina.detections_per_img";
+            const int64_t mv[4] = {B, K, N, N};
+            for (int j = 0; j < 4; ++j) m.i[j] = mv[j];
+            for (int j = 0; j < 5; ++j) m.p[j] = P.ref(crec[j]);
+            m.p[5] = P.ref(rbuf);
+            m.p[6] = P.ref(P.out_box);
+            m.p[7] = P.ref(P.out_score);
+            m.p[8] = P.ref(P.out_label);
+            m.p[9] = P.ref(P.out_count);
+            P.add(m);
+        }
+        P.input = bd.inp;
+        P.dets = DETS;
+        return Pp;
+    }
+
+  private:
+    void gn(const std::string& p, WRef* g = nullptr, WRef* b = nullptr) {
+        const Params& Pm = pk_.params();
+        std::vector<float> w(256, 0.f), bb(256, 0.f);
+        if (pk_.values()) {
+            std::memcpy(w.data(), Pm.get(p + ".weight", 256), 1024);
+            std::memcpy(bb.data(), Pm.get(p + ".bias", 256), 1024);
+        }
+        WRef rg = pk_.raw("gn:" + p + ".weight", w), rb = pk_.raw("gn:" + p + ".bias", bb);
+        if (g) *g = rg;
+        if (b) *b = rb;
+    }
 };
 
 // ------------------------------------------------------------------------------------ engine cache
@@ -1317,8 +1678,11 @@ struct Engine {
     Params params;
     std::unique_ptr<SSDLite> ssd;
     std::unique_ptr<FasterRCNN> frcnn;
+    std::unique_ptr<RetinaNet> retina;
     std::map<std::tuple<int, int, int, bool>, std::unique_ptr<Plan>> plans;
+    uint64_t clock = 0;
 };
+constexpr size_t PLAN_CACHE = 64;
 
 static std::unique_ptr<Engine> make_engine(const Config& c, const Params* values, Pack* pack_out) {
     auto e = std::make_unique<Engine>();
@@ -1329,9 +1693,12 @@ static std::unique_ptr<Engine> make_engine(const Config& c, const Params* values
     if (c.kind == 0) {
         e->ssd = std::make_unique<SSDLite>(c, *e->packer);
         e->ssd->pack_all();
-    } else {
+    } else if (c.kind == 1) {
         e->frcnn = std::make_unique<FasterRCNN>(c, *e->packer);
         e->frcnn->pack_all();
+    } else {
+        e->retina = std::make_unique<RetinaNet>(c, *e->packer);
+        e->retina->pack_all();
     }
     return e;
 }
@@ -1349,17 +1716,26 @@ static Engine* engine(const Config& c) {
 static Plan* plan_for(Engine* e, int B, int H, int W, bool u8) {
     auto key = std::make_tuple(B, H, W, u8);
     auto it = e->plans.find(key);
-    if (it != e->plans.end()) return it->second.get();
-    std::unique_ptr<Plan> p = e->cfg.kind == 0 ? e->ssd->lower(B, H, W, u8) : e->frcnn->lower(B, H, W, u8);
+    if (it != e->plans.end()) {
+        it->second->last_use = ++e->clock;
+        return it->second.get();
+    }
+    if (e->plans.size() >= PLAN_CACHE) {  // evict the least recently used plan
+        auto lru = e->plans.begin();
+        for (auto i = e->plans.begin(); i != e->plans.end(); ++i)
+            if (i->second->last_use < lru->second->last_use) lru = i;
+        e->plans.erase(lru);
+    }
+    std::unique_ptr<Plan> p = e->cfg.kind == 0   ? e->ssd->lower(B, H, W, u8)
+                              : e->cfg.kind == 1 ? e->frcnn->lower(B, H, W, u8)
+                                                 : e->retina->lower(B, H, W, u8);
     p->finalize();
+    p->last_use = ++e->clock;
     Plan* raw = p.get();
     e->plans[key] = std::move(p);
     return raw;
 }
 
-struct External {
-    uint64_t weights = 0, workspace = 0, images = 0, count = 0, boxes = 0, scores = 0, labels = 0;
-};
 
 static std::vector<edgedet_op> records(const Plan& P, const External& x) {
     std::vector<edgedet_op> out(P.ops.size());
@@ -1408,7 +1784,8 @@ using namespace edgedet::lower;
     }
 
 static int config_of(int32_t kind, int32_t num_classes, int32_t reduced_tail, Config* c) {
-    EDGEDET_REQUIRE(kind == EDGEDET_MODEL_SSDLITE || kind == EDGEDET_MODEL_FRCNN, "unknown model kind");
+    EDGEDET_REQUIRE(kind == EDGEDET_MODEL_SSDLITE || kind == EDGEDET_MODEL_FRCNN || kind == EDGEDET_MODEL_RETINANET,
+                    "unknown model kind");
     EDGEDET_REQUIRE(num_classes >= 2 && num_classes <= 1024, "num_classes must be 2..1024");
     c->kind = kind;
     c->num_classes = num_classes;
@@ -1521,19 +1898,78 @@ extern "C" int edgedet_model_forward(int32_t kind, int32_t num_classes, int32_t 
     Config c;
     if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
     EDGEDET_REQUIRE(weights && images && workspace && count && boxes && scores && labels, "model_forward: null pointer");
-    std::vector<edgedet_op> recs;
+    std::shared_ptr<const std::vector<edgedet_op>> recs;
     EDGEDET_TRY({
         std::lock_guard<std::mutex> g(g_mu);
         Plan* p = plan_for(engine(c), B, H, W, input_u8 != 0);
         External x{(uint64_t)weights, (uint64_t)workspace, (uint64_t)images, (uint64_t)count, (uint64_t)boxes,
                    (uint64_t)scores, (uint64_t)labels};
-        recs = records(*p, x);
+        if (!p->resolved || !(p->resolved_for == x)) {  // resolved once per set of pointers, not per call
+            p->resolved = std::make_shared<const std::vector<edgedet_op>>(records(*p, x));
+            p->resolved_for = x;
+        }
+        recs = p->resolved;
     })
-    return edgedet_plan_run(recs.data(), (int64_t)recs.size(), stream);
+    // issued outside the lock: calls on different streams run concurrently
+    return edgedet_plan_run(recs->data(), (int64_t)recs->size(), stream);
+}
+
+extern "C" int64_t edgedet_model_buffers(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                                         int32_t W, int32_t input_u8, edgedet_buffer* out, int64_t cap) {
+    Config c;
+    if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
+    EDGEDET_TRY({
+        std::lock_guard<std::mutex> g(g_mu);
+        Plan* p = plan_for(engine(c), B, H, W, input_u8 != 0);
+        const int64_t n = (int64_t)p->bufs.size();
+        if (out && cap >= n) {
+            for (int64_t k = 0; k < n; ++k) {
+                const Buf& b = p->bufs[(size_t)k];
+                edgedet_buffer& r = out[k];
+                std::memset(&r, 0, sizeof(r));
+                std::strncpy(r.name, b.name.c_str(), sizeof(r.name) - 1);
+                r.offset = b.off;
+                r.nbytes = b.nbytes;
+                r.dtype = b.dtype;
+                r.ndim = (int32_t)std::min<size_t>(b.shape.size(), 6);
+                for (int j = 0; j < r.ndim; ++j) r.shape[j] = b.shape[(size_t)j];
+            }
+        }
+        return n;
+    })
+}
+
+extern "C" int64_t edgedet_model_op_names(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B,
+                                          int32_t H, int32_t W, int32_t input_u8, char* out, int64_t cap) {
+    Config c;
+    if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
+    EDGEDET_TRY({
+        std::lock_guard<std::mutex> g(g_mu);
+        Plan* p = plan_for(engine(c), B, H, W, input_u8 != 0);
+        std::string all;
+        for (size_t k = 0; k < p->ops.size(); ++k) all += (k ? "\n" : "") + p->ops[k].name;
+        const int64_t need = (int64_t)all.size() + 1;
+        if (out && cap >= need) std::memcpy(out, all.c_str(), (size_t)need);
+        return need;
+    })
+}
+
+extern "C" int edgedet_model_release(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                                     int32_t W, int32_t input_u8) {
+    Config c;
+    if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
+    EDGEDET_TRY({
+        std::lock_guard<std::mutex> g(g_mu);
+        engine(c)->plans.erase(std::make_tuple(B, H, W, input_u8 != 0));
+        return 0;
+    })
 }
 
 extern "C" int edgedet_model_max_detections(int32_t kind) {
-    return kind == EDGEDET_MODEL_SSDLITE ? SSDLite::DETS : (kind == EDGEDET_MODEL_FRCNN ? FasterRCNN::BOX_DETS : -1);
+    return kind == EDGEDET_MODEL_SSDLITE     ? SSDLite::DETS
+           : kind == EDGEDET_MODEL_FRCNN     ? FasterRCNN::BOX_DETS
+           : kind == EDGEDET_MODEL_RETINANET ? RetinaNet::DETS
+                                             : -1;
 }
 
 // ---- the per-model names of SURVEY.md §8(b)

@@ -16,7 +16,7 @@ import torch
 
 from . import ops
 
-KIND = {"ssd": 0, "faster_rcnn": 1, "frcnn": 1}
+KIND = {"ssd": 0, "faster_rcnn": 1, "frcnn": 1, "retinanet": 2}
 
 
 def _kind(name):
@@ -72,6 +72,43 @@ def records(kind, B, H, W, weights, workspace, num_classes=91, reduced_tail=True
     if m != n:
         ops.check(int(m) if m < 0 else -1)
     return rec
+
+
+BUFFER_DTYPE = np.dtype([("name", "S96"), ("offset", "<i8"), ("nbytes", "<i8"), ("dtype", "<i4"), ("ndim", "<i4"),
+                         ("shape", "<i8", 6)])
+
+
+def buffers(kind, B, H, W, num_classes=91, reduced_tail=True, u8=False):
+    """The plan's workspace buffers (edgedet_model_buffers): name, offset, nbytes, dtype, ndim, shape."""
+    L = ops.lib()
+    args = (_kind(kind), num_classes, int(bool(reduced_tail)), B, H, W, int(u8))
+    n = L.edgedet_model_buffers(*args, None, 0)
+    if n < 0:
+        ops.check(int(n))
+    out = np.zeros(int(n), dtype=BUFFER_DTYPE)
+    m = L.edgedet_model_buffers(*args, out.ctypes.data, int(n))
+    if m != n:
+        ops.check(int(m) if m < 0 else -1)
+    return out
+
+
+def op_names(kind, B, H, W, num_classes=91, reduced_tail=True, u8=False):
+    """The layer name of every record of the plan (edgedet_model_op_names)."""
+    L = ops.lib()
+    args = (_kind(kind), num_classes, int(bool(reduced_tail)), B, H, W, int(u8))
+    n = L.edgedet_model_op_names(*args, None, 0)
+    if n < 0:
+        ops.check(int(n))
+    buf = ctypes.create_string_buffer(int(n))
+    m = L.edgedet_model_op_names(*args, buf, int(n))
+    if m != n:
+        ops.check(int(m) if m < 0 else -1)
+    return buf.value.decode().split("\n")
+
+
+def release(kind, B, H, W, num_classes=91, reduced_tail=True, u8=False):
+    """Drop the library's cached lowering of this shape (it is rebuilt on next use)."""
+    ops.check(ops.lib().edgedet_model_release(_kind(kind), num_classes, int(bool(reduced_tail)), B, H, W, int(u8)))
 
 
 class NativeDetector:

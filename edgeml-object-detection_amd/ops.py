@@ -6,6 +6,7 @@ library binds to the same HIP runtime (libamdhip64.so.7) that PyTorch-ROCm alrea
 device pointers / streams from torch tensors are valid inside the library.
 """
 import ctypes
+import math
 import os
 
 import numpy as np
@@ -23,6 +24,7 @@ FORK, JOIN, SSD_POSTPROCESS = 15, 16, 17
 GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 SSD_STEM = 21
 MBCONV = 22
+WAIT = 23
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
@@ -50,7 +52,9 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_model_weights_size", "edgedet_model_pack", "edgedet_model_workspace_size", "edgedet_model_prepare",
            "edgedet_model_prepare_host", "edgedet_model_forward", "edgedet_model_max_detections",
            "edgedet_model_records", "edgedet_ssdlite_workspace_size", "edgedet_ssdlite_forward",
-           "edgedet_frcnn_workspace_size", "edgedet_frcnn_forward")
+           "edgedet_frcnn_workspace_size", "edgedet_frcnn_forward", "edgedet_plan_check", "edgedet_release_lanes",
+           "edgedet_lane_sets", "edgedet_nms_workspace_size", "edgedet_nms_ws", "edgedet_batched_nms_ws",
+           "edgedet_topk_segments", "edgedet_box_decode", "edgedet_model_buffers", "edgedet_model_op_names", "edgedet_model_release")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -79,11 +83,20 @@ def lib():
     except OSError as e:
         raise EdgeDetUnavailable(f"cannot load {LIB_PATH}: {e}") from e
     L.edgedet_plan_run.argtypes = [_vp, _i64, _vp]
+    L.edgedet_plan_check.argtypes = [_vp, _i64]
+    L.edgedet_release_lanes.argtypes = [_vp]
+    L.edgedet_lane_sets.restype = _i64
     L.edgedet_graph_create.argtypes = [_vp, _i64, _vp, ctypes.POINTER(_vp)]
     L.edgedet_graph_launch.argtypes = [_vp, _vp]
     L.edgedet_graph_destroy.argtypes = [_vp]
     L.edgedet_nms.argtypes = [_vp, _vp, _i64, _dbl, _vp, _vp, _vp]
     L.edgedet_batched_nms.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp]
+    L.edgedet_nms_workspace_size.argtypes = [_i64]
+    L.edgedet_nms_workspace_size.restype = _i64
+    L.edgedet_nms_ws.argtypes = [_vp, _vp, _i64, _dbl, _vp, _vp, _vp, _i64, _vp]
+    L.edgedet_batched_nms_ws.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp, _i64, _vp]
+    L.edgedet_topk_segments.argtypes = [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]
+    L.edgedet_box_decode.argtypes = [_vp, _vp, _i64, _flt, _flt, _flt, _flt, _flt, _flt, _flt, _vp, _vp]
     L.edgedet_roi_align.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _flt, _i32, _i32, _i32, _vp, _vp]
     L.edgedet_conv2d.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                                  _vp, _vp]
@@ -113,6 +126,11 @@ def lib():
     L.edgedet_model_records.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _u64, _u64, _u64, _u64, _u64, _u64,
                                         _u64, _vp, _i64]
     L.edgedet_model_records.restype = _i64
+    L.edgedet_model_buffers.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64]
+    L.edgedet_model_buffers.restype = _i64
+    L.edgedet_model_op_names.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.c_char_p, _i64]
+    L.edgedet_model_op_names.restype = _i64
+    L.edgedet_model_release.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32, _i32]
     L.edgedet_ssdlite_workspace_size.argtypes = [_i32, _i32, _i32, _i32, _i32, _i32]
     L.edgedet_ssdlite_workspace_size.restype = _i64
     L.edgedet_ssdlite_forward.argtypes = [_vp, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
@@ -176,9 +194,39 @@ def batched_nms(boxes, scores, idxs, iou_threshold):
     n = int(scores.shape[0])
     keep = torch.empty(max(n, 1), dtype=torch.int64, device=scores.device)
     nk = torch.zeros(1, dtype=torch.int32, device=scores.device)
-    check(lib().edgedet_batched_nms(_ptr(boxes), _ptr(scores), _ptr(idxs), n, float(iou_threshold), _ptr(keep),
-                                    _ptr(nk), stream_handle()))
+    L = lib()
+    wb = int(L.edgedet_nms_workspace_size(n))
+    if wb < 0:
+        check(wb)
+    ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=scores.device)  # scratch from torch's allocator
+    check(L.edgedet_batched_nms_ws(_ptr(boxes), _ptr(scores), _ptr(idxs), n, float(iou_threshold), _ptr(keep),
+                                   _ptr(nk), _ptr(ws), wb, stream_handle()))
     return keep[:int(nk.item())]
+
+
+def topk_segments(values, seg_off, k):
+    """torch.topk per segment values[seg_off[s]:seg_off[s+1]] -> (values [S,k], index in segment [S,k],
+    count [S]); descending, ties lower index first."""
+    _need_cuda(values, seg_off)
+    S = int(seg_off.shape[0]) - 1
+    ov = torch.zeros((max(S, 1), k), dtype=torch.float32, device=values.device)
+    oi = torch.full((max(S, 1), k), -1, dtype=torch.int64, device=values.device)
+    oc = torch.zeros(max(S, 1), dtype=torch.int32, device=values.device)
+    check(lib().edgedet_topk_segments(_ptr(values), _ptr(seg_off), S, int(k), _ptr(ov), _ptr(oi), _ptr(oc),
+                                      stream_handle()))
+    return ov[:S], oi[:S], oc[:S]
+
+
+def box_decode(deltas, ref_boxes, weights, clamp=math.log(1000.0 / 16), image_size=None):
+    """BoxCoder.decode_single (+ clip_boxes_to_image when image_size = (h, w) is given)."""
+    _need_cuda(deltas, ref_boxes)
+    n = int(deltas.shape[0])
+    out = torch.empty((n, 4), dtype=torch.float32, device=deltas.device)
+    h, w = image_size if image_size is not None else (0.0, 0.0)
+    wx, wy, ww, wh = (float(v) for v in weights)
+    check(lib().edgedet_box_decode(_ptr(deltas), _ptr(ref_boxes), n, wx, wy, ww, wh, float(clamp), float(h), float(w),
+                                   _ptr(out), stream_handle()))
+    return out
 
 
 def roi_align_nhwc(feat_nhwc, rois, spatial_scale, output_size=7, sampling_ratio=2):

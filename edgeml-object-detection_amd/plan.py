@@ -1,14 +1,18 @@
 """Static execution plans: the host side of the engine.
 
-A detector forward for a fixed (batch, height, width) is lowered once into
+A detector forward for a fixed (batch, height, width) is, in the library (csrc/lower.hip), lowered
+once into
   * a packed weight blob (BatchNorm folded in float64, conv weights K-contiguous
-    [Cout][KH][KW][Cin] with K padded to 32, depthwise weights tap-major [K*K][C], SE fc weights
-    transposed), uploaded once per model and shared by every plan of that model;
-  * one device arena (a single torch allocation, 256-byte aligned carve-outs) holding every
-    activation, the NHWC input staging buffer and the output buffers;
+    [Cout][KH][KW][Cin] with K padded to 32 plus their bf16 planes, depthwise weights tap-major
+    [K*K][C], SE fc weights transposed), uploaded once per model and shared by every plan of it;
+  * one workspace (256-byte aligned carve-outs) holding every activation, the input staging buffer
+    and the output buffers;
   * an array of edgedet_op records (numpy, layout = include/edgedet.h) that libedgedet.so runs
     directly or captures into a hipGraph replayed per batch.
-Nothing here computes detections: every FLOP runs in the HIP kernels of libedgedet.so.
+NativePlan is that plan on the Python side: the workspace as one torch allocation, the records
+resolved against it, and the named buffers.  Plan / conv_op below build records by hand for the
+unit tests of single kernels.  Nothing here computes detections: every FLOP runs in the HIP kernels
+of libedgedet.so.
 """
 import ctypes
 import os
@@ -255,6 +259,10 @@ class Plan:
         """Issue the following ops on lane k (0 = the caller's stream)."""
         self._lane = k
 
+    def wait(self, lane, on):
+        """Lane `lane` waits for everything issued so far on lane `on` (both forked, or 0)."""
+        self.ops.append(Op(ops.WAIT, {0: lane, 1: on}, name=f"wait{lane}<-{on}"))
+
     def join(self):
         self._lane = 0
         self.ops.append(Op(ops.JOIN, {0: self._forked}, name="join"))
@@ -334,6 +342,99 @@ class Plan:
             kinds[op.kind] = kinds.get(op.kind, 0) + 1
         return {"ops": len(self.ops), "by_kind": kinds, "arena_MB": self.arena_bytes / 2 ** 20,
                 "weights_MB": self.weights.size * 4 / 2 ** 20}
+
+
+# ------------------------------------------------------------------------------ native plans
+_DTYPES = {0: torch.float32, 1: torch.int32, 2: torch.int64, 3: torch.uint8, 4: torch.int16}
+
+
+class NativeBuf:
+    """A named carve-out of a NativePlan's workspace (edgedet_model_buffers)."""
+
+    def __init__(self, plan, name, offset, nbytes, dtype, shape):
+        self.plan, self.name, self.off, self.nbytes = plan, name, int(offset), int(nbytes)
+        self.dtype, self.shape = dtype, tuple(int(v) for v in shape)
+
+    def ptr(self):
+        return self.plan.arena.data_ptr() + self.off
+
+    def tensor(self):
+        es = _esize(self.dtype)
+        n = int(np.prod(self.shape))
+        return self.plan.arena[self.off:self.off + n * es].view(self.dtype).view(self.shape)
+
+
+class NativePlan:
+    """The library's plan of (model, B, H, W, u8): workspace, resolved records, named buffers."""
+
+    def __init__(self, model, B, H, W, u8, device):
+        from . import native
+        self.model, self.B, self.H, self.W, self.u8 = model, B, H, W, u8
+        self.device = torch.device(device)
+        kind, nc, rt = model.kind, model.num_classes, model.reduced_tail
+        self.weights = model.weights(self.device)
+        self.arena = torch.zeros(native.workspace_size(kind, B, H, W, nc, rt, u8), dtype=torch.uint8,
+                                 device=self.device)
+        L = ops.lib()
+        if self.device.type == "cuda":
+            ops.check(L.edgedet_model_prepare(native._kind(kind), nc, int(rt), B, H, W, int(u8),
+                                              self.arena.data_ptr(), ops.stream_handle()))
+        else:
+            host = np.zeros(self.arena.numel(), np.uint8)
+            ops.check(L.edgedet_model_prepare_host(native._kind(kind), nc, int(rt), B, H, W, int(u8),
+                                                   host.ctypes.data, host.size))
+            self.arena.copy_(torch.from_numpy(host))
+        self.records = native.records(kind, B, H, W, self.weights.data_ptr(), self.arena.data_ptr(), nc, rt, u8)
+        self.buffers = {}
+        for b in native.buffers(kind, B, H, W, nc, rt, u8):
+            name = bytes(b["name"]).split(b"\0", 1)[0].decode()
+            self.buffers[name] = NativeBuf(self, name, b["offset"], b["nbytes"], _DTYPES[int(b["dtype"])],
+                                           b["shape"][:int(b["ndim"])])
+        names = native.op_names(kind, B, H, W, nc, rt, u8)
+        by_ptr = {}
+        for nb in self.buffers.values():
+            by_ptr.setdefault(nb.ptr(), nb)
+        self.ops = []
+        for k, r in enumerate(self.records):
+            op = Op(int(r["kind"]), {j: int(v) for j, v in enumerate(r["i"])},
+                    {j: (by_ptr.get(int(v), int(v)) if v else None) for j, v in enumerate(r["p"])},
+                    {j: float(v) for j, v in enumerate(r["f"])}, {j: float(v) for j, v in enumerate(r["d"])},
+                    name=names[k], lane=int(r["i"][ops.LANE_FIELD]))
+            self.ops.append(op)
+        self.input = self.buffer("images")
+        self.out_box, self.out_score = self.buffer("out.boxes"), self.buffer("out.scores")
+        self.out_label, self.out_count = self.buffer("out.labels"), self.buffer("out.count")
+        pre = next(op for op in self.ops if op.kind == ops.PREPROCESS)
+        self.resized = tuple(int(pre.i[j]) for j in (3, 4, 5, 6))  # (Ho, Wo, Hp, Wp) of the transform
+        self.graph = None
+        model.attach(self)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def buffer(self, name):
+        try:
+            return self.buffers[name]
+        except KeyError:
+            raise KeyError(f"plan has no buffer {name!r}") from None
+
+    def finalize(self):
+        return self
+
+    @property
+    def arena_bytes(self):
+        return self.arena.numel()
+
+    run = Plan.run
+    capture = Plan.capture
+    replay = Plan.replay
+    __del__ = Plan.__del__
+
+    def summary(self):
+        kinds = {}
+        for op in self.ops:
+            kinds[op.kind] = kinds.get(op.kind, 0) + 1
+        return {"ops": len(self.ops), "by_kind": kinds, "arena_MB": self.arena_bytes / 2 ** 20,
+                "weights_MB": self.weights.numel() / 2 ** 20}
 
 
 # ------------------------------------------------------------------------------ op helpers

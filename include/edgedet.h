@@ -68,7 +68,8 @@ enum {
     EDGEDET_OP_RETINA_SELECT = 19,/* RetinaNet per (image, level): sigmoid > t, top-k, decode, clip   */
     EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
     EDGEDET_OP_SSD_STEM = 21,     /* SSDLite features.0.0 + features.0.1 in one pass                  */
-    EDGEDET_OP_MBCONV = 22        /* InvertedResidual without SE: expand, depthwise, project, residual */
+    EDGEDET_OP_MBCONV = 22,       /* InvertedResidual without SE: expand, depthwise, project, residual */
+    EDGEDET_OP_WAIT = 23          /* lane i[0] waits for everything issued so far on lane i[1]         */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,
@@ -77,8 +78,15 @@ enum {
 #define EDGEDET_OP_LANE 47
 #define EDGEDET_MAX_LANES 4
 
-/* Run ops[0..n) on `stream`.  Shapes are checked on the host before any launch. */
+/* Run ops[0..n) on `stream`.  Shapes are checked on the host before any launch; the lane topology
+ * (FORK / JOIN / WAIT and every record's lane) is checked before anything is issued. */
 int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream);
+/* The lane-topology check alone (no device access): 0 or the error edgedet_plan_run would return. */
+int edgedet_plan_check(const edgedet_op* ops, int64_t n);
+/* Drop the side lanes (streams + events) the library keeps for `stream` (at most 16 sets are kept,
+ * least recently used evicted; a set in use by a running call is destroyed when that call returns). */
+int edgedet_release_lanes(void* stream);
+int64_t edgedet_lane_sets(void);
 
 /* Capture ops[0..n) into a hipGraph (instantiated); *graph receives an opaque handle. */
 int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** graph);
@@ -92,7 +100,8 @@ int edgedet_graph_destroy(void* graph);
  * the same static plan the Python host builds (edgeml_amd/models.py; results bit-identical to it).
  *   kind         EDGEDET_MODEL_SSDLITE (ssdlite320_mobilenet_v3_large, detect.py:24/26; reduced_tail
  *                1 = the COCO-pretrained variant, 0 = the --model-path / train.py variant) or
- *                EDGEDET_MODEL_FRCNN (fasterrcnn_resnet50_fpn_v2, detect.py:30/32; reduced_tail unused)
+ *                EDGEDET_MODEL_FRCNN (fasterrcnn_resnet50_fpn_v2, detect.py:30/32; reduced_tail unused) or
+ *                EDGEDET_MODEL_RETINANET (retinanet_resnet50_fpn_v2, detect.py:36/38, the CLI's third model)
  *   num_classes  91 (coco) or 21 (voc), detect.py:67
  * Weights: edgedet_model_pack packs torchvision-named host tensors (a state_dict: names, fp32 values,
  * element counts; num_batches_tracked may be omitted) into a blob of edgedet_model_weights_size bytes
@@ -102,10 +111,10 @@ int edgedet_graph_destroy(void* graph);
  * caller-owned device memory of edgedet_model_workspace_size bytes for (B, H, W, input_u8), set up
  * once by edgedet_model_prepare (zeroes it and writes the anchors / rescale constants; synchronous).  Outputs:
  * count [B] int32, boxes [B][K][4] xyxy float in original pixels, scores [B][K] descending,
- * labels [B][K] int64, K = edgedet_model_max_detections(kind) (300 SSD / 100 FRCNN), the first
+ * labels [B][K] int64, K = edgedet_model_max_detections(kind) (300 SSD / 100 FRCNN / 300 RetinaNet), the first
  * count[b] rows valid (detect.py:79-81).  forward is asynchronous on `stream`.
  */
-enum { EDGEDET_MODEL_SSDLITE = 0, EDGEDET_MODEL_FRCNN = 1 };
+enum { EDGEDET_MODEL_SSDLITE = 0, EDGEDET_MODEL_FRCNN = 1, EDGEDET_MODEL_RETINANET = 2 };
 int64_t edgedet_model_weights_size(int32_t kind, int32_t num_classes, int32_t reduced_tail);
 int edgedet_model_pack(int32_t kind, int32_t num_classes, int32_t reduced_tail, int64_t n_params,
                        const char* const* names, const float* const* host_values, const int64_t* numels,
@@ -123,6 +132,28 @@ int edgedet_model_forward(int32_t kind, int32_t num_classes, int32_t reduced_tai
                           void* workspace, int32_t* count, float* boxes, float* scores, int64_t* labels,
                           void* stream);
 int edgedet_model_max_detections(int32_t kind);
+/* The workspace buffers of the plan (name, byte offset into the workspace, element type, shape): what a
+ * host reads back for inspection (the parity tests read the head outputs, scores, proposals ...).
+ * Returns the buffer count; fills out[] when cap is large enough. */
+enum { EDGEDET_DT_F32 = 0, EDGEDET_DT_I32 = 1, EDGEDET_DT_I64 = 2, EDGEDET_DT_U8 = 3, EDGEDET_DT_I16 = 4 };
+typedef struct edgedet_buffer {
+    char name[96];
+    int64_t offset;  /* bytes from the workspace base */
+    int64_t nbytes;
+    int32_t dtype;   /* EDGEDET_DT_* */
+    int32_t ndim;
+    int64_t shape[6];
+} edgedet_buffer;
+int64_t edgedet_model_buffers(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                              int32_t W, int32_t input_u8, edgedet_buffer* out, int64_t cap);
+/* The layer name of every record ('\n'-separated, torchvision module paths): returns the bytes needed
+ * (including the terminating NUL); fills out when cap is large enough. */
+int64_t edgedet_model_op_names(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H,
+                               int32_t W, int32_t input_u8, char* out, int64_t cap);
+/* Drop the cached plan of (B, H, W, input dtype) (at most 64 plans per model are kept, least recently
+ * used evicted; records and workspaces already handed out stay valid). */
+int edgedet_model_release(int32_t kind, int32_t num_classes, int32_t reduced_tail, int32_t B, int32_t H, int32_t W,
+                          int32_t input_u8);
 /* The op records forward would run (for graph capture: edgedet_graph_create on them, and for tests);
  * pointers resolved against the given bases (0 = the workspace's own region for images / outputs).
  * Returns the record count; fills out[] when cap is large enough. */
@@ -146,17 +177,43 @@ int edgedet_frcnn_forward(const void* weights, int32_t num_classes, const void* 
  * torchvision::nms (reference call sites: SSD postprocess, RPN filter_proposals and RoIHeads
  * postprocess_detections, all reached from detect.py:78; semantics SURVEY.md App. A.0).
  * boxes [n,4], scores [n] -> keep [n] int64 (indices, score-descending, ties lower index first),
- * *d_num_keep int32.  n <= 1024.  Suppress j when inter/(area_i+area_j-inter) > iou_threshold.
+ * *d_num_keep int32.  Suppress j when inter/(area_i+area_j-inter) > iou_threshold.  n <= 524288:
+ * up to 1024 boxes one workgroup does it all; above, a radix sort, a tiled IoU bitmask and a blocked
+ * greedy scan (csrc/unitops.hip), with scratch from the stream-ordered allocator (hipMallocAsync on
+ * `stream`); the _ws variants take caller-owned scratch of edgedet_nms_workspace_size(n) bytes instead.
  */
 int edgedet_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
                 int64_t* keep, int32_t* d_num_keep, void* stream);
 
 /*
  * torchvision::ops.batched_nms (per-group greedy NMS; result sorted by score descending, ties by
- * lower index).  Equivalent to the reference's _batched_nms_vanilla.  n <= 1024.
+ * lower index).  Equivalent to the reference's _batched_nms_vanilla.  n <= 524288 (as edgedet_nms).
  */
 int edgedet_batched_nms(const float* boxes, const float* scores, const int64_t* idxs, int64_t n,
                         double iou_threshold, int64_t* keep, int32_t* d_num_keep, void* stream);
+int64_t edgedet_nms_workspace_size(int64_t n);
+int edgedet_nms_ws(const float* boxes, const float* scores, int64_t n, double iou_threshold, int64_t* keep,
+                   int32_t* d_num_keep, void* workspace, int64_t workspace_bytes, void* stream);
+int edgedet_batched_nms_ws(const float* boxes, const float* scores, const int64_t* idxs, int64_t n,
+                           double iou_threshold, int64_t* keep, int32_t* d_num_keep, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+
+/*
+ * torch.topk per segment (RPN filter_proposals' per-level pre_nms_top_n, SSD's per-class topk of
+ * postprocess_detections; reached from detect.py:78): segment s is values[seg_off[s] .. seg_off[s+1]);
+ * out_values / out_index [nseg][k] (index within the segment), out_count[s] = min(k, length).  Values
+ * descending, ties lower index first (the rule the oracle fixes).  1 <= k <= 1024.
+ */
+int edgedet_topk_segments(const float* values, const int64_t* seg_off, int64_t nseg, int32_t k,
+                          float* out_values, int64_t* out_index, int32_t* out_count, void* stream);
+
+/*
+ * torchvision BoxCoder.decode_single: deltas [n,4] against ref_boxes [n,4] (xyxy)
+ * with weights (wx, wy, ww, wh), dw / dh clamped to <= clamp (log(1000/16) in torchvision); then
+ * clip_boxes_to_image to [0, img_w] x [0, img_h] when both are > 0.  out [n,4]; 16-byte aligned rows.
+ */
+int edgedet_box_decode(const float* deltas, const float* ref_boxes, int64_t n, float wx, float wy, float ww,
+                       float wh, float clamp, float img_h, float img_w, float* out, void* stream);
 
 /*
  * torchvision::roi_align forward, aligned=False (MultiScaleRoIAlign's call),

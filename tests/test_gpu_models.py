@@ -80,21 +80,23 @@ def test_model_call_equals_plan_outputs(ssd):
         assert bool((g["scores"][:-1] >= g["scores"][1:]).all())
 
 
-def test_ssd_batch_chains_agree(ssd):
+def test_ssd_batch_chains_agree(ssd, monkeypatch):
     """A batch lowered as concurrent sub-batch chains (stream lanes) against one chain: tile choices
     depend on the per-chain batch, so summation orders (not results) may differ.  Both run against
     the oracle with the full protocol."""
     from edgeml_amd import synthetic
     sd, model = ssd
     imgs = synthetic.make_batch(16, 640, 640, seed=61)
+    from edgeml_amd import native
     reps = {}
     for n in (1, 2):
-        model.CHAINS = n
+        monkeypatch.setenv("EDGEDET_SSD_CHAINS", str(n))  # read by the library's lowering
+        native.release("ssd", 16, 640, 640)
         model.plans.clear()
         plan = _run(model, imgs)
         assert plan.chains == n
         reps[n] = PM.ssd_check(plan, sd, 91, True, imgs, f"ssd b=16 chains={n}", own_check=0)
         print(reps[n])
-    model.CHAINS = type(model).CHAINS
+    native.release("ssd", 16, 640, 640)
     model.plans.clear()
     assert reps[1]["rows"] == reps[2]["rows"] == 16 * 300

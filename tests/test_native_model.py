@@ -1,73 +1,157 @@
-"""The model-level C-ABI's lowering (csrc/lower.hip) against the Python host's (models.py, plan.py),
-on the CPU: the native library must build the identical plan — the same packed weight bytes, the
-same workspace size and constants, and byte-identical op records (every shape, tile, pointer,
-threshold and lane) — so a non-Python host running edgedet_model_forward runs exactly what the
-Python model object runs (tests/test_gpu_native_model.py then checks the detections on the GPU).
+"""The library's lowering (csrc/lower.hip, the only one: the Python model objects run its plans) against
+independent host restatements, on the CPU:
+  * weight packing (edgedet_model_pack): BatchNorm folding in float64, the (kh, kw, ci) K order padded
+    to 32, the three bf16 planes, depthwise tap-major weights, FC6's (c, h, w) -> (h, w, c) permutation,
+    the predictor's [bbox | cls] rows, GroupNorm affine parameters, at the offsets the records use;
+  * plan constants (edgedet_model_prepare_host): the anchors against edgeml_amd.anchors (pinned to the
+    oracle's generators in tests/test_host.py) and the rescale ratios;
+  * state_dict validation.
+tests/test_gpu_native_model.py runs the same plans through the pure C-ABI on the GPU.
 """
 import numpy as np
 import pytest
 import torch
 
+from edgeml_amd import anchors as anc
 from edgeml_amd import models, native, ops, synthetic
-
-
-def _python_plan(model, B, H, W, u8):
-    P = model.build_plan(B, H, W, u8)  # device None -> the plan finalises on the CPU
-    P.finalize()
-    return P
-
-
-CASES = [
-    ("ssd", 91, True, 2, 480, 640, False),
-    ("ssd", 91, True, 16, 640, 640, True),    # two batch chains on stream lanes
-    ("ssd", 21, False, 3, 427, 640, False),   # full tail, VOC classes
-    ("faster_rcnn", 91, True, 1, 480, 640, False),
-    ("faster_rcnn", 21, True, 2, 612, 612, True),
-    ("faster_rcnn", 91, True, 1, 427, 640, True),  # fp32 resize scale: 799 x 1199
-]
+from edgeml_amd.plan import fold_bn, pack_conv_weight, pack_dw_weight, split_bf16x3
 
 
 @pytest.fixture(scope="module")
 def built():
     cache = {}
 
-    def get(kind, nc, rt):
+    def get(kind, nc=91, rt=True):
         key = (kind, nc, rt)
         if key not in cache:
             sd = synthetic.synthetic_state_dict(kind, nc, rt, seed=3, calibrated=False)
-            m = models.SSDLite320(sd, nc, rt) if kind == "ssd" else models.FasterRCNNFPNv2(sd, nc)
+            cls = {"ssd": models.SSDLite320, "faster_rcnn": models.FasterRCNNFPNv2,
+                   "retinanet": models.RetinaNetFPNv2}[kind]
+            m = cls(sd, nc, rt) if kind == "ssd" else cls(sd, nc)
             cache[key] = (sd, m)
         return cache[key]
     return get
 
 
-@pytest.mark.parametrize("kind,nc,rt", [("ssd", 91, True), ("ssd", 21, False), ("faster_rcnn", 91, True)])
-def test_packed_weights_identical(built, kind, nc, rt):
-    sd, m = built(kind, nc, rt)
-    blob = native.pack_state_dict(kind, sd, nc, rt)
-    host = m.pack.upload("cpu").numpy().view(np.uint8)
-    assert blob.size == host.size == native.weights_size(kind, nc, rt)
-    assert np.array_equal(blob, host)
+def _np(t):
+    return t.detach().cpu().to(torch.float64).numpy()
 
 
-@pytest.mark.parametrize("kind,nc,rt,B,H,W,u8", CASES)
-def test_records_and_constants_identical(built, kind, nc, rt, B, H, W, u8):
-    sd, m = built(kind, nc, rt)
-    P = _python_plan(m, B, H, W, u8)
-    ws = native.workspace_size(kind, B, H, W, nc, rt, u8)
-    assert ws == P.arena_bytes
-    rec = native.records(kind, B, H, W, P.weights.device_blob.data_ptr(), P.arena.data_ptr(), nc, rt, u8)
-    assert len(rec) == len(P.records)
-    for k, (a, b) in enumerate(zip(rec, P.records)):
-        assert a.tobytes() == b.tobytes(), (k, P.ops[k].name, a, b)
-    host = np.zeros(ws, np.uint8)
-    ops.check(ops.lib().edgedet_model_prepare_host(native._kind(kind), nc, int(rt), B, H, W, int(u8),
-                                                   host.ctypes.data, ws))
-    assert np.array_equal(host, P.arena.numpy())  # constants at the same offsets, nothing else written
+def _blob_f32(m, ptr, n):
+    """n floats of the packed blob at a record's weight pointer (CPU plans point into the model's
+    blob tensor)."""
+    off = ptr - m.weights("cpu").data_ptr()
+    assert off % 4 == 0 and 0 <= off < m.blob.size
+    return m.blob[off:off + 4 * n].view(np.float32)
+
+
+def _op(P, name):
+    return next(op for op in P.ops if op.name == name)
+
+
+def _check_conv(m, op, w_oihw, b, cin_pad=None):
+    wp, K, Kpad, _ = pack_conv_weight(w_oihw, cin_pad)
+    cout = wp.shape[0]
+    assert op.i[12] == K and op.i[13] == Kpad
+    np.testing.assert_array_equal(_blob_f32(m, op.p[1], cout * Kpad), wp.reshape(-1))
+    np.testing.assert_array_equal(_blob_f32(m, op.p[2], cout), np.asarray(b, np.float32))
+    planes = _blob_f32(m, op.p[6], (3 * cout * Kpad + 1) // 2).view(np.uint16)[:3 * cout * Kpad]
+    np.testing.assert_array_equal(planes, split_bf16x3(wp).reshape(-1))
+
+
+@pytest.mark.parametrize("rt", [True, False])
+def test_ssd_packing_matches_restatement(built, rt):
+    sd, m = built("ssd", 91 if rt else 21, rt)
+    P = m.build_plan(2, 320, 320)
+    s = lambda k: _np(sd[k])  # noqa: E731
+    p = "backbone.features.0.2.block.0"  # expand 1x1 + BN (eps 1e-3)
+    w, b = fold_bn(s(p + ".0.weight"), s(p + ".1.weight"), s(p + ".1.bias"), s(p + ".1.running_mean"),
+                   s(p + ".1.running_var"), 1e-3)
+    _check_conv(m, _op(P, p), w, b)
+    p = "backbone.features.0.2.block.1"  # depthwise, tap-major
+    w, b = fold_bn(s(p + ".0.weight"), s(p + ".1.weight"), s(p + ".1.bias"), s(p + ".1.running_mean"),
+                   s(p + ".1.running_var"), 1e-3)
+    op = _op(P, p)
+    np.testing.assert_array_equal(_blob_f32(m, op.p[1], w.size), pack_dw_weight(w).reshape(-1))
+    np.testing.assert_array_equal(_blob_f32(m, op.p[2], b.size), b)
+    p = "head.classification_head.module_list.0.1"  # 1x1 with bias, no BN
+    _check_conv(m, _op(P, p), s(p + ".weight").astype(np.float32), s(p + ".bias"))
+    p = "backbone.features.0.4.block.2"  # SqueezeExcitation: fc1 [S][C], fc2 transposed [S][C]
+    op = _op(P, p)
+    C, S = op.i[1], op.i[2]
+    np.testing.assert_array_equal(_blob_f32(m, op.p[1], S * C), s(p + ".fc1.weight").astype(np.float32).reshape(-1))
+    np.testing.assert_array_equal(_blob_f32(m, op.p[3], S * C),
+                                  s(p + ".fc2.weight")[:, :, 0, 0].T.astype(np.float32).reshape(-1))
+
+
+def test_frcnn_packing_matches_restatement(built):
+    sd, m = built("faster_rcnn")
+    P = m.build_plan(1, 480, 640)
+    s = lambda k: _np(sd[k])  # noqa: E731
+    q = "backbone.body."
+    w, b = fold_bn(s(q + "conv1.weight"), s(q + "bn1.weight"), s(q + "bn1.bias"), s(q + "bn1.running_mean"),
+                   s(q + "bn1.running_var"), 1e-5)
+    _check_conv(m, _op(P, q + "conv1.weight"), w, b, cin_pad=4)
+    w6 = s("roi_heads.box_head.5.weight").astype(np.float32).reshape(1024, 256, 7, 7).transpose(0, 2, 3, 1)
+    _check_conv(m, _op(P, "roi_heads.box_head.5"), w6.reshape(1024, -1)[:, :, None, None],
+                s("roi_heads.box_head.5.bias"))
+    pr = "roi_heads.box_predictor."
+    wp = np.concatenate([s(pr + "bbox_pred.weight"), s(pr + "cls_score.weight")], 0).astype(np.float32)
+    bp = np.concatenate([s(pr + "bbox_pred.bias"), s(pr + "cls_score.bias")], 0)
+    _check_conv(m, _op(P, "roi_heads.box_predictor"), wp[:, :, None, None], bp)
+
+
+def test_retinanet_packing_matches_restatement(built):
+    sd, m = built("retinanet")
+    P = m.build_plan(1, 480, 640)
+    s = lambda k: _np(sd[k])  # noqa: E731
+    q = "head.classification_head.conv.0."
+    _check_conv(m, _op(P, q + "0@0"), s(q + "0.weight").astype(np.float32), np.zeros(256))  # no bias
+    gn = _op(P, q + "1@0")
+    np.testing.assert_array_equal(_blob_f32(m, gn.p[1], 256), s(q + "1.weight").astype(np.float32))
+    np.testing.assert_array_equal(_blob_f32(m, gn.p[2], 256), s(q + "1.bias").astype(np.float32))
+    p = "backbone.fpn.extra_blocks.p7"
+    op = _op(P, p + ".weight")
+    assert op.i[24] == 1  # relu(P6) applied by P7's input load
+    _check_conv(m, op, s(p + ".weight").astype(np.float32), s(p + ".bias"))
+
+
+def _const(P, name):
+    return P.buffer(name).tensor().numpy()
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 480, 640), (1, 427, 640)])
+def test_plan_constants_match_restatement(built, B, H, W):
+    _, ssd = built("ssd")
+    P = ssd.build_plan(B, H, W)
+    np.testing.assert_array_equal(_const(P, "anchors"), anc.ssd_default_boxes(ssd.grids, (320, 320)))
+    np.testing.assert_array_equal(_const(P, "ratio"),
+                                  np.tile(np.float32([np.float32(W) / np.float32(320), np.float32(H) / np.float32(320)]),
+                                          (B, 1)))
+    _, fr = built("faster_rcnn")
+    P = fr.build_plan(B, H, W)
+    Ho, Wo, Hp, Wp = P.resized
+    assert (Ho, Wo) == fr.resized_size(H, W)
+    grids = [tuple(f.shape[1:3]) for f in P.feats]
+    for lvl, a in enumerate(anc.rpn_anchors(grids, (Hp, Wp))):
+        np.testing.assert_array_equal(_const(P, f"rpn.anchors@{lvl}"), a)
+    np.testing.assert_array_equal(_const(P, "ratio"), np.tile(np.float32([np.float32(W) / np.float32(Wo),
+                                                                           np.float32(H) / np.float32(Ho)]), (B, 1)))
+    _, rn = built("retinanet")
+    P = rn.build_plan(B, H, W)
+    _, _, Hp, Wp = P.resized
+    na = P.level_anchors
+    sel = next(op for op in P.ops if op.kind == ops.RETINA_SELECT)
+    grids = []
+    for lvl in range(len(na)):
+        conv = _op(P, f"head.classification_head.cls_logits@{lvl}")
+        grids.append((conv.i[4], conv.i[5]))
+    assert [gh * gw * 9 for gh, gw in grids] == na and sel.i[2] == sum(na)
+    np.testing.assert_array_equal(_const(P, "anchors"), np.concatenate(anc.retina_anchors(grids, (Hp, Wp)), 0))
 
 
 def test_pack_rejects_bad_state_dict(built):
-    sd, _ = built("ssd", 91, True)
+    sd, _ = built("ssd")
     bad = dict(sd)
     bad.pop("head.regression_head.module_list.5.1.bias")
     with pytest.raises(ops.EdgeDetError, match="missing parameter"):
@@ -78,15 +162,27 @@ def test_pack_rejects_bad_state_dict(built):
         native.pack_state_dict("ssd", bad, 91, True)
 
 
-def test_records_identical_with_fused_blocks(built, monkeypatch):
-    """The opt-in whole-block MBCONV lowering (EDGEDET_MB_BLOCK=1) is mirrored by the native host."""
-    sd, m = built("ssd", 91, True)
-    monkeypatch.setattr(models, "MB_BLOCK_FUSE", True)
+def test_fused_block_lowering(built, monkeypatch):
+    """The opt-in whole-block MBCONV lowering (EDGEDET_MB_BLOCK=1) replaces blocks 0.2 and 0.3."""
+    _, m = built("ssd")
     monkeypatch.setenv("EDGEDET_MB_BLOCK", "1")
-    B, H, W = 5, 300, 400  # a shape no other test lowers (the native host caches plans per shape)
-    P = _python_plan(m, B, H, W, False)
+    B, H, W = 5, 300, 400  # a shape no other test lowers (the library caches plans per shape)
+    native.release("ssd", B, H, W)
+    P = m.build_plan(B, H, W)
     assert sum(op.kind == ops.MBCONV for op in P.ops) == 2
-    rec = native.records("ssd", B, H, W, P.weights.device_blob.data_ptr(), P.arena.data_ptr(), 91, True, False)
-    assert len(rec) == len(P.records)
-    for k, (a, b) in enumerate(zip(rec, P.records)):
-        assert a.tobytes() == b.tobytes(), (k, P.ops[k].name)
+    native.release("ssd", B, H, W)
+
+
+def test_model_records_entry_resolves_external_pointers(built):
+    """edgedet_model_records with caller-owned images / outputs (the graph-capture path of a foreign
+    host): those records point there, every other pointer into the workspace or the weights."""
+    _, m = built("faster_rcnn")
+    B, H, W = 1, 480, 640
+    ext = [0x10000000 * (k + 1) for k in range(5)]
+    rec = native.records("faster_rcnn", B, H, W, 0x7000000000, 0x8000000000, 91, True, False, images=ext[0],
+                         outputs=tuple(ext[1:]))
+    P = m.build_plan(B, H, W)
+    assert len(rec) == len(P.records) and (rec["kind"] == P.records["kind"]).all()
+    assert ext[0] in set(int(v) for v in rec[0]["p"])
+    merge = rec[-1]
+    assert [int(merge["p"][j]) for j in (6, 7, 8, 9)] == [ext[2], ext[3], ext[4], ext[1]]
