@@ -603,9 +603,6 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(ConvParams p, int ncg) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
-#ifndef X6_PF
-#define X6_PF 1
-#endif
 constexpr int BK6 = 16;
 constexpr int LDR6 = 24;  // padded LDS row, in bf16
 
@@ -821,24 +818,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
             }
     };
-#if X6_PF == 2
-    // Two stages of register prefetch: stage k+2's global loads are issued before stage k's MFMAs,
-    // stage k+1 (loaded one step earlier) is split and stored to LDS after them.
-    load_stage(r0, 0);
-    store_stage(r0, 0);
-    __syncthreads();
-    if (nk > 1) load_stage(r0, BK6);
-    auto step = [&](int kc, Regs& hold, Regs& next) {
-        if (kc + 2 < nk) load_stage(next, (kc + 2) * BK6);
-        compute(kc & 1);
-        if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
-        __syncthreads();
-    };
-    for (int kc = 0; kc < nk; kc += 2) {
-        step(kc, r0, r1);
-        if (kc + 1 < nk) step(kc + 1, r1, r0);
-    }
-#else
     load_stage(r0, 0);
     store_stage(r0, 0);
     __syncthreads();
@@ -848,7 +827,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
         if (kc + 1 < nk) store_stage(r0, (kc & 1) ^ 1);
         __syncthreads();
     }
-#endif
 
     conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
 }
@@ -858,27 +836,6 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 // row bits 2..3 (chunk' = chunk ^ ((row >> 2) & 3)): the four lane groups of a ds_read_b128 then hit
 // 16 distinct 16-B slots of the 256-B bank row (conflict-free), and the double-buffered image of the
 // three A and three B planes fits 144 KiB (one block of 8 waves per CU, two waves per SIMD).
-#ifndef X6B_PF
-#define X6B_PF 1
-#endif
-#ifndef X6B_PIPE
-#define X6B_PIPE 1
-#endif
-#ifndef X6B_IGLP
-#define X6B_IGLP 3
-#endif
-#ifndef X6B_BRANCHLESS
-#define X6B_BRANCHLESS 0
-#endif
-#ifndef X6B_STAGGER
-#define X6B_STAGGER 0
-#endif
-#ifndef X6B_GLDS
-#define X6B_GLDS 1
-#endif
-#ifndef X6B_MF16
-#define X6B_MF16 1
-#endif
 constexpr int BK6B = 32;
 constexpr int X3Z = 32;  // leading zero elements of a pre-split scratch (16-B aligned planes follow)
 
@@ -898,13 +855,13 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // (!UT) the chunks past Cin are zeroed (they meet the zero weight padding).
 // BN = 64 (with BM = 128, the skewed 16x16x32 pipeline and LDS-DMA B only): 4 x 2 waves of 32 x 32
 // for the Cout = 64 layers, which a 128-wide N tile computes half empty; waves 0..3 copy the B rows.
-template <bool XF, bool UT, bool PS, int BM = 256, int PF = X6B_PF, bool P1 = false, int BN = 128>
+template <bool XF, bool UT, bool PS, int BM = 256, int PF = 1, bool P1 = false, int BN = 128>
 __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
     static_assert(!P1 || !PS, "pointwise stages: fp32 input");
-    constexpr bool GL = X6B_GLDS && PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
-    static_assert(BN == 128 || (BN == 64 && BM == 128 && GL && X6B_MF16 && !PS), "x6b BN = 64: 128 x 64, LDS-DMA B, 16x16x32");
+    constexpr bool GL = PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
+    static_assert(BN == 128 || (BN == 64 && BM == 128 && GL && !PS), "x6b BN = 64: 128 x 64, LDS-DMA B");
     constexpr int WM = BN == 64 ? 4 : (BM == 256 ? 4 : 2), WN = 8 / WM, TM = BM / (WM * 32), TN = BN / (WN * 32), NT = 512;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
     constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
@@ -994,9 +951,9 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
         kw = sk.kw;
         ci0 = sk.ci;
     };
-    auto load_part = [&](Regs& R, const StageK& sk, int bbuf, bool la, bool lb) {
+    auto load_stage = [&](Regs& R, const StageK& sk, int bbuf) {
         const int k0 = sk.k0;
-        if (GL && lb && 16 * wid < BN) {
+        if (GL && 16 * wid < BN) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
             // -> the 16-B slot l of the block); the swizzle is applied on the source address
             const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 2) & 3);
@@ -1008,8 +965,7 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
                     (const __attribute__((address_space(1))) void*)(src + pl * wplane),
                     (__attribute__((address_space(3))) void*)(Bs + bbuf * 3 * PB + pl * PB + 16 * wid * BK6B), 16, 0, 0);
         }
-        if (!la) {
-        } else if constexpr (PS) {
+        if constexpr (PS) {
             int kh, kw, ci0;
             stage_tap(sk, kh, kw, ci0);
             if constexpr (GL) {
@@ -1060,22 +1016,15 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
             const float* xt = p.x + (int64_t)(kh * p.W + kw) * p.x_pstride + ci;
 #pragma unroll
             for (int j = 0; j < AJ; ++j) {
-                // branch-free (a padding tap loads from p.x and is zeroed), so the stage is one
-                // basic block the scheduler can interleave
+                // (a branch-free form, padding taps loading from p.x and zeroed, measured 3-5% slower)
                 const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
                 const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-#if X6B_BRANCHLESS
-                f32x4 v = *reinterpret_cast<const f32x4*>(ok ? xt + a_base[j] : p.x);
-                if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
-                R.a[j] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-#else
                 f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (ok) {
                     v = *reinterpret_cast<const f32x4*>(xt + a_base[j]);
                     if constexpr (XF) v = in_transform(p, v, a_b[j], ci);
                 }
                 R.a[j] = v;
-#endif
             }
         } else {
             const int k = k0 + c8 * 4;
@@ -1095,13 +1044,12 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
                 R.a[j] = v;
             }
         }
-        if (!GL && lb) {
+        if (!GL) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
                 R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
         }
     };
-    auto load_stage = [&](Regs& R, const StageK& sk, int bbuf) { load_part(R, sk, bbuf, true, true); };
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
@@ -1131,14 +1079,6 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint4*>(Bb + pl * PB + o) = R.b[pl];
     };
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int nk_all = p.Kpad / BK6B;
     const int kbeg = ksp > 1 ? (blockIdx.x & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
@@ -1178,58 +1118,14 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
         }
         return sk;
     };
-    Cursor cb = ca;  // the B rows' cursor (runs behind ca in the late wave group of the stagger)
     const int h = lane >> 5;
     const int l32 = lane & 31;
-    struct Frags {
-        bf16x8 a[TM][3], b[TN][3];
-    };
-    // Fragments of K half s (16 of the stage's 32) of LDS buffer buf.
-    auto read_frags = [&](Frags& F, int buf, int s) {
-        const unsigned short* A = As + buf * 3 * PA;
-        const unsigned short* Bb = Bs + buf * 3 * PB;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int o = swz64(wave_m * TM * 32 + i * 32 + l32, 2 * s + h);
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) F.a[i][pl] = *reinterpret_cast<const bf16x8*>(A + pl * PA + o);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int o = swz64(wave_n * TN * 32 + j * 32 + l32, 2 * s + h);
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) F.b[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
-        }
-    };
-    // smallest terms first: (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
-    auto mfmas = [&](const Frags& F) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][2], F.b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][1], F.b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][2], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][1], F.b[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[i][0], F.b[j][0], acc[i][j], 0, 0, 0);
-            }
-    };
-    auto compute = [&](int buf) {
-        Frags F;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            read_frags(F, buf, s);
-            mfmas(F);
-        }
-    };
-    // 16x16x32 form (X6B_MF16): the wave's 32TM x 32TN tile as (2TM) x (2TN) 16x16 C tiles, each MFMA
-    // taking the whole 32-deep stage (lane l: row l & 15, k chunk l >> 4 of the swizzled 64-B row).
-    // Under load the chip holds a higher clock for this shape than for 32x32x16 at the same cycles per
-    // FLOP (MI355X_MICROARCH.md, DVFS item 7).  A fragment half is TM row blocks (or TN column blocks)
-    // of 16, so a stage's MFMAs fall into four quadrants (row half, column half); quadrant (1, 1) is
-    // carried across the barrier in F1, which takes the place of the K-half skew of the 32x32 form:
-    // after the barrier the matrix pipe runs it while the next stage's first fragments are read.
+    // 16x16x32 form: the wave's 32TM x 32TN tile as (2TM) x (2TN) 16x16 C tiles, each MFMA taking the
+    // whole 32-deep stage (lane l: row l & 15, k chunk l >> 4 of the swizzled 64-B row).  Under load
+    // the chip holds a higher clock for this shape than for 32x32x16 at the same cycles per FLOP
+    // (MI355X_MICROARCH.md, DVFS item 7; FRCNN 311 -> 329 img/s same-box).  A fragment half is TM row
+    // blocks (or TN column blocks) of 16, so a stage's MFMAs fall into four quadrants (row half,
+    // column half).
     struct F16 {
         bf16x8 a[TM][3], b[TN][3];
     };
@@ -1255,7 +1151,8 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
             for (int pl = 0; pl < 3; ++pl) F.b[u][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
         }
     };
-    // quadrant (ha, hb) from the A half in FA and the B half in FB; smallest terms first, as mfmas()
+    // quadrant (ha, hb) from the A half in FA and the B half in FB; smallest terms first:
+    // (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
     auto mfma16 = [&](const F16& FA, const F16& FB, int ha, int hb) {
 #pragma unroll
         for (int t = 0; t < TM; ++t)
@@ -1270,154 +1167,59 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][0], c, 0, 0, 0);
             }
     };
-    // back to the 32x32 block view of the epilogue: block (i, j) register 4(2ii + jj) + r
-    auto epilogue16 = [&]() {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = acc4[2 * i + (q >> 1)][2 * j + (q & 1)][r];
-        conv_epilogue<TM, TN, true>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
-    };
-    if constexpr (X6B_MF16 && PF != 2 && X6B_PIPE) {
-    Regs r0;
-    F16 F0, F1;
-    load_stage(r0, next_k(ca), 0);
-    store_stage(r0, 0);
-    __syncthreads();
-    if (nk > 1) load_stage(r0, next_k(ca), 1);
-    read16(F0, 0, 0);
-    read16(F1, 0, 1);
-    mfma16(F0, F0, 0, 0);
-    mfma16(F0, F1, 0, 1);
-    mfma16(F1, F0, 1, 0);
-    if (nk > 1) store_stage(r0, 1);
-    __syncthreads();
-    for (int kc = 1; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
-        read16(F0, buf, 0);
-        __builtin_amdgcn_sched_barrier(0);  // issue the reads before the carried quadrant that hides them
-        mfma16(F1, F1, 1, 1);
-        __builtin_amdgcn_sched_barrier(0);  // F1 is rewritten only after the carried quadrant issued
-        read16(F1, buf, 1);
+    if constexpr (PF != 2) {
+        // Skewed pipeline: quadrant (1, 1) of stage k-1 is carried across the barrier in F1, so after
+        // the barrier the matrix pipe runs it while stage k's first fragments are read; stage k+1's
+        // operands are written to the other buffer under stage k's MFMAs.
+        Regs r0;
+        F16 F0, F1;
+        load_stage(r0, next_k(ca), 0);
+        store_stage(r0, 0);
+        __syncthreads();
+        if (nk > 1) load_stage(r0, next_k(ca), 1);
+        read16(F0, 0, 0);
+        read16(F1, 0, 1);
         mfma16(F0, F0, 0, 0);
         mfma16(F0, F1, 0, 1);
         mfma16(F1, F0, 1, 0);
-        store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
-#if X6B_IGLP
-#pragma unroll
-        for (int i = 0; i < TM * TN * 18; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x002, X6B_IGLP, 0);  // VALU
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-        }
-#endif
+        if (nk > 1) store_stage(r0, 1);
         __syncthreads();
-    }
-    mfma16(F1, F1, 1, 1);
-    epilogue16();
-    return;
-    } else if constexpr (PF != 2 && X6B_PIPE) {
-    // Skewed pipeline: the second K half of stage k-1 (fragments held in registers across the
-    // barrier) runs while stage k's first-half fragments are read, and stage k+1's operands are
-    // written to the other buffer under stage k's MFMAs, so the matrix pipe does not idle through
-    // the read latency after each barrier.
-#if X6B_STAGGER
-    // Stagger: the two waves that share a SIMD (w and w + 4) would otherwise run in lockstep, both in
-    // their MFMAs and both in their split/stores at the same time.  Waves 4..7 store stage k+1 (A
-    // loaded one stage earlier, still a full stage of latency) at the start of stage k, then load
-    // stage k+2's A rows; waves 0..3 keep the load-early / store-late order.  Same LDS image and
-    // barriers, so results are unchanged.  Measured slower on every arrangement (box head 3x3, tile
-    // 25: 2.29 ms lockstep; 2.56 late-store group; 2.46 / 2.47 mid-store in waves 4..7 / 0..3), so
-    // off by default (X6B_STAGGER=0).
-    const bool upper = __builtin_amdgcn_readfirstlane(wid) >= 4;
-    const bool late = X6B_STAGGER == 1 && GL && !PS && upper;
-    // (2 / 3: waves 4..7 / 0..3 store between the two MFMA halves instead)
-    const bool mid = (X6B_STAGGER == 2 && upper) || (X6B_STAGGER == 3 && !upper);
-#else
-    const bool late = false, mid = false;
-#endif
-    Regs r0;
-    Frags F0, F1;
-    load_stage(r0, next_k(ca), 0);
-    (void)next_k(cb);
-    store_stage(r0, 0);
-    if (late && nk > 1) load_part(r0, next_k(ca), 0, true, false);
-    __syncthreads();
-    if (nk > 1) {
-        if (late) {
-            load_part(r0, next_k(cb), 1, false, true);
-            store_stage(r0, 1);
-            if (nk > 2) load_part(r0, next_k(ca), 0, true, false);
-        } else {
-            load_stage(r0, next_k(ca), 1);
-            (void)next_k(cb);
-        }
-    }
-    read_frags(F0, 0, 0);
-    mfmas(F0);
-    read_frags(F1, 0, 1);
-    if (!late && nk > 1) store_stage(r0, 1);
-    __syncthreads();
-    for (int kc = 1; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (late) {
-            if (kc + 1 < nk) {
-                load_part(r0, next_k(cb), buf ^ 1, false, true);
-                store_stage(r0, buf ^ 1);
+        for (int kc = 1; kc < nk; ++kc) {
+            const int buf = kc & 1;
+            if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
+            read16(F0, buf, 0);
+            __builtin_amdgcn_sched_barrier(0);  // issue the reads before the carried quadrant that hides them
+            mfma16(F1, F1, 1, 1);
+            __builtin_amdgcn_sched_barrier(0);  // F1 is rewritten only after the carried quadrant issued
+            read16(F1, buf, 1);
+            mfma16(F0, F0, 0, 0);
+            mfma16(F0, F1, 0, 1);
+            mfma16(F1, F0, 1, 0);
+            store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+            // Spread the split VALU, the LDS writes of stage k+1 and the fragment reads over the gaps
+            // of the MFMAs (1 MFMA : 1 LDS read : 3 VALU : 1 LDS write; 0 groups cost FRCNN 3%, 1..5
+            // VALU within 1%) instead of letting them bunch up after the last MFMA.
+#pragma unroll
+            for (int i = 0; i < TM * TN * 18; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
             }
-            if (kc + 2 < nk) load_part(r0, next_k(ca), buf ^ 1, true, false);
-        } else if (kc + 1 < nk) {
-            load_stage(r0, next_k(ca), buf ^ 1);
+            __syncthreads();
         }
-        read_frags(F0, buf, 0);
-        __builtin_amdgcn_sched_barrier(0);  // issue the reads before the MFMAs that hide them
-        mfmas(F1);
-        if (mid && kc + 1 < nk) store_stage(r0, buf ^ 1);
-#if X6B_PIPE == 2
-        store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
-        mfmas(F0);
-        read_frags(F1, buf, 1);
-#else
-#if X6B_IGLP
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        mfmas(F0);
-        read_frags(F1, buf, 1);
-        if (!late && !mid) store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
-#if X6B_IGLP
-        // Spread the split VALU, the LDS writes of stage k+1 and the fragment reads of the second
-        // half over the gaps of the second half's 24 MFMAs (an MFMA gap hides about 24 cycles of
-        // vector issue) instead of letting them bunch up after the last MFMA.
-#pragma unroll
-        for (int i = 0; i < TM * TN * 6; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x002, X6B_IGLP, 0);  // VALU
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-        }
-#endif
-#endif
+        mfma16(F1, F1, 1, 1);
+    } else {
+        // Two register stages: stage k+2's global loads are issued before stage k's MFMAs, stage k+1's
+        // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
+        // time to land.
+        Regs r0, r1;
+        load_stage(r0, next_k(ca), 0);
+        store_stage(r0, 0);
+        if (nk > 1) load_stage(r1, next_k(ca), 1);
         __syncthreads();
-    }
-    mfmas(F1);
-    } else if constexpr (PF == 2) {
-    // Two register stages: stage k+2's global loads are issued before stage k's MFMAs, stage k+1's
-    // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
-    // time to land.
-    Regs r0, r1;
-    load_stage(r0, next_k(ca), 0);
-    store_stage(r0, 0);
-    if (nk > 1) load_stage(r1, next_k(ca), 1);
-    __syncthreads();
-    auto step = [&](int kc, Regs& hold, Regs& next) {
-        if (kc + 2 < nk) load_stage(next, next_k(ca), kc & 1);  // (no LDS-DMA with two register stages)
-        if constexpr (X6B_MF16) {  // the four quadrants of the 16x16x32 form, no carry
+        auto step = [&](int kc, Regs& hold, Regs& next) {
+            if (kc + 2 < nk) load_stage(next, next_k(ca), kc & 1);  // (no LDS-DMA with two register stages)
             F16 F0, F1;
             read16(F0, kc & 1, 0);
             read16(F1, kc & 1, 1);
@@ -1425,35 +1227,25 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
             mfma16(F0, F1, 0, 1);
             mfma16(F1, F0, 1, 0);
             mfma16(F1, F1, 1, 1);
-        } else {
-            compute(kc & 1);
+            if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
+            __syncthreads();
+        };
+        for (int kc = 0; kc < nk; kc += 2) {
+            step(kc, r1, r0);
+            if (kc + 1 < nk) step(kc + 1, r0, r1);
         }
-        if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
-        __syncthreads();
-    };
-    for (int kc = 0; kc < nk; kc += 2) {
-        step(kc, r1, r0);
-        if (kc + 1 < nk) step(kc + 1, r0, r1);
     }
-    if constexpr (X6B_MF16) {
-        epilogue16();
-        return;
-    }
-    } else {
-    Regs r0;
-    load_stage(r0, next_k(ca), 0);
-    store_stage(r0, 0);
-    __syncthreads();
-    for (int kc = 0; kc < nk; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
-        compute(buf);
-        if (kc + 1 < nk) store_stage(r0, buf ^ 1);
-        __syncthreads();
-    }
-    }
-
-    conv_epilogue<TM, TN>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
+    // back to the 32x32 block view of the epilogue: block (i, j) register 4(2ii + jj) + r
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = acc4[2 * i + (q >> 1)][2 * j + (q & 1)][r];
+    conv_epilogue<TM, TN, true>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
 }
 
 // Pre-split of a conv input for the PS tile: out[pl][pix][c] (three dense bf16 planes, the RN split
@@ -1500,7 +1292,7 @@ static bool x6b_p1() {
     return v;
 }
 
-template <int BM = 256, int PF = X6B_PF, int BN = 128>
+template <int BM = 256, int PF = 1, int BN = 128>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     const ConvParams& p = p0;
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");

@@ -429,24 +429,18 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
 // Side streams and fork/join/wait events, one set per (device, caller stream), shared by every
 // thread (cgo and other foreign hosts call from arbitrary OS threads): two plans in flight on two
 // caller streams (run_batches) get disjoint side lanes, so their lane work overlaps instead of
-// queueing on one shared side stream.  The cache is bounded (LANE_CACHE sets, least recently used
-// evicted; edgedet_release_lanes drops a stream's set at once); a set is destroyed when the last run
-// using it returns.  Every WAIT record of a run gets its own event (no event is re-recorded while a
-// wait on it may be pending in the same capture).
+// queueing on one shared side stream.  At most LANE_CACHE sets exist: a new caller stream beyond that
+// takes over the least recently used set (re-keyed, never destroyed: the HIP runtime's captured graphs
+// keep references to the streams and events they were captured with, and destroying them measured
+// a segfault in a later hipGraphLaunch).  A set's mutex serialises issue into it, so two threads whose
+// caller streams share a set still record and wait its events in a consistent order.
 struct Lanes {
     hipStream_t side[EDGEDET_MAX_LANES] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t join_ev[EDGEDET_MAX_LANES] = {};
     std::vector<hipEvent_t> wait_ev;
     uint64_t last_use = 0;
-    ~Lanes() {
-        for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
-            if (side[l]) (void)hipStreamDestroy(side[l]);
-            if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
-        }
-        if (fork_ev) (void)hipEventDestroy(fork_ev);
-        for (hipEvent_t e : wait_ev) (void)hipEventDestroy(e);
-    }
+    std::mutex mu;
     bool ensure_wait_events(size_t n) {
         while (wait_ev.size() < n) {
             hipEvent_t e = nullptr;
@@ -458,21 +452,21 @@ struct Lanes {
 };
 constexpr size_t LANE_CACHE = 16;
 static std::mutex g_lanes_mu;
-static std::map<std::pair<int, hipStream_t>, std::shared_ptr<Lanes>> g_lanes_by_stream;
+static std::map<std::pair<int, hipStream_t>, Lanes*> g_lanes_by_stream;  // sets live for the process
 static uint64_t g_lanes_clock = 0;
 
-static std::shared_ptr<Lanes> make_lanes() {
-    auto L = std::make_shared<Lanes>();  // a partial set is destroyed by ~Lanes on the failure paths
+static Lanes* make_lanes() {
+    auto* L = new Lanes();
     for (int l = 1; l < EDGEDET_MAX_LANES; ++l) {
         if (hipStreamCreateWithFlags(&L->side[l], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&L->join_ev[l], hipEventDisableTiming) != hipSuccess)
-            return nullptr;
+            return nullptr;  // (a partial set is leaked: creation failing means the device is unusable)
     }
     if (hipEventCreateWithFlags(&L->fork_ev, hipEventDisableTiming) != hipSuccess) return nullptr;
     return L;
 }
 
-static std::shared_ptr<Lanes> lanes_for(hipStream_t caller) {
+static Lanes* lanes_for(hipStream_t caller) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     const auto key = std::make_pair(dev, caller);
@@ -482,13 +476,19 @@ static std::shared_ptr<Lanes> lanes_for(hipStream_t caller) {
         it->second->last_use = ++g_lanes_clock;
         return it->second;
     }
-    auto L = make_lanes();
-    if (!L) return nullptr;
-    if (g_lanes_by_stream.size() >= LANE_CACHE) {  // evict the least recently used set
-        auto lru = g_lanes_by_stream.begin();
+    Lanes* L = nullptr;
+    size_t on_dev = 0;
+    for (auto& kv : g_lanes_by_stream) on_dev += kv.first.first == dev;
+    if (on_dev >= LANE_CACHE) {  // take over the least recently used set of this device
+        auto lru = g_lanes_by_stream.end();
         for (auto i = g_lanes_by_stream.begin(); i != g_lanes_by_stream.end(); ++i)
-            if (i->second->last_use < lru->second->last_use) lru = i;
-        g_lanes_by_stream.erase(lru);  // destroyed now, or when a run still holding it returns
+            if (i->first.first == dev && (lru == g_lanes_by_stream.end() || i->second->last_use < lru->second->last_use))
+                lru = i;
+        L = lru->second;
+        g_lanes_by_stream.erase(lru);
+    } else {
+        L = make_lanes();
+        if (!L) return nullptr;
     }
     L->last_use = ++g_lanes_clock;
     g_lanes_by_stream[key] = L;
@@ -533,16 +533,16 @@ static int64_t check_topology(const edgedet_op* ops, int64_t n) {
     return waits;
 }
 
-// own: the lane set to issue on (a graph capture passes its own, see edgedet_graph_create); null = the
-// cached set of the caller stream.
-static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s, std::shared_ptr<Lanes> own = nullptr) {
+static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
     const int64_t waits = check_topology(ops, n);
     if (waits < 0) return (int)waits;
     bool need_lanes = false;
     for (int64_t k = 0; k < n && !need_lanes; ++k)
         need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
-    std::shared_ptr<Lanes> lanes = !need_lanes ? nullptr : own ? own : lanes_for(s);
+    Lanes* lanes = need_lanes ? lanes_for(s) : nullptr;
     EDGEDET_REQUIRE(!need_lanes || lanes, "could not create the side lanes (streams / events)");
+    std::unique_lock<std::mutex> issue;
+    if (lanes) issue = std::unique_lock<std::mutex>(lanes->mu);
     EDGEDET_REQUIRE(!waits || lanes->ensure_wait_events((size_t)waits), "could not create the wait events");
     auto lane_stream = [&](int64_t l) { return l == 0 ? s : lanes->side[l]; };
     int64_t wait_k = 0;
@@ -573,14 +573,9 @@ static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s, std::shared_
     return 0;
 }
 
-// A captured plan with its own lane set (side streams + fork / join / wait events, fresh per capture):
-// the HIP runtime's captured graph keeps references to the streams and events it was captured with
-// (destroying them, by evicting a cached lane set or right after the capture, measured: a segfault in
-// the next hipGraphLaunch), so they live exactly as long as the graph, and no two graphs share one.
 struct Graph {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
-    std::shared_ptr<Lanes> lanes;
 };
 
 }  // namespace edgedet
@@ -600,7 +595,8 @@ extern "C" int edgedet_release_lanes(void* stream) {
     int dev = 0;
     EDGEDET_CHECK_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(g_lanes_mu);
-    g_lanes_by_stream.erase(std::make_pair(dev, (hipStream_t)stream));
+    auto it = g_lanes_by_stream.find(std::make_pair(dev, (hipStream_t)stream));
+    if (it != g_lanes_by_stream.end()) it->second->last_use = 0;  // first to be taken over
     return 0;
 }
 
@@ -614,16 +610,6 @@ extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stre
         if (w < 0) return (int)w;
     }
     Graph* g = new Graph();
-    bool need_lanes = false;
-    for (int64_t k = 0; k < n && !need_lanes; ++k)
-        need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
-    if (need_lanes) {
-        g->lanes = make_lanes();
-        if (!g->lanes) {
-            delete g;
-            EDGEDET_REQUIRE(false, "graph_create: could not create the side lanes (streams / events)");
-        }
-    }
     {
         const hipError_t eb = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
         if (eb != hipSuccess) {
@@ -632,7 +618,7 @@ extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stre
             return -2;
         }
     }
-    const int rc = run_ops(ops, n, s, g->lanes);
+    const int rc = run_ops(ops, n, s);
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &graph);
     if (rc != 0) {

@@ -7,7 +7,9 @@ Behaviour kept from the reference (detect.py:62-106): images are taken in sorted
 read as RGB and scaled by 1/255, every image gets one ``<name[:-4]>.npy`` (N,6) float64 file
 ``[cls, xc, yc, w, h, conf]`` normalised by the original size, rows in score order, an empty result
 still writes a (0,6) file.  Differences: images of equal size are batched across the whole list
-(results are per image and identical to batch=1) and decoded by a thread pool ahead of the engine,
+(results are per image and identical to batch=1) and decoded ahead of the engine (baseline JPEGs:
+Huffman decoding on a host thread pool, IDCT / upsampling / colour conversion on the GPU, csrc/jpeg.hip,
+byte-identical to the host decoder; other files on the host),
 and under ``torchrun`` the single-process run's batch list is split into contiguous blocks of
 batches, one per GPU (so every file is byte-identical whatever the GPU count), with the output rows
 gathered to rank 0 over RCCL (distributed.py).
@@ -96,32 +98,56 @@ def image_sizes(dataset, workers=None):
         return list(ex.map(_image_size, paths))
 
 
-def _decoded_batches(dataset, chunks, sizes, workers=None):
-    """Yield (names, (H, W), uint8 [B,3,H,W] pinned batch) for the given batches of equal-size images
-    (lists of dataset indices, distributed.size_batches).  Each image is decoded straight into its
-    slot of the batch's pinned buffer (the engine uploads it as is) on a thread pool (one thread per
-    usable host core; PIL releases the GIL while decoding), with the next two batches in flight while
-    the caller uses the current one."""
+def _packet_or_none(path):
+    """The device-decode packet of a JPEG file (csrc/jpeg.hip; entropy decode on this host thread, the
+    GIL released inside the library), or None when the file is not a JPEG the device path handles."""
+    from . import jpeg
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:2] != b"\xff\xd8":
+        return None
+    pk, _ = jpeg.packet(data)
+    return pk
+
+
+def _decoded_batches(dataset, chunks, sizes, workers=None, device_decode=True):
+    """Yield (names, (H, W), batch) for the given batches of equal-size images (lists of dataset
+    indices, distributed.size_batches).  With device_decode, a batch whose files are all JPEGs the
+    device decoder handles is a jpeg.Packets (entropy-decoded on the host threads, reconstructed on
+    the GPU by run_batches straight into the plan's input, byte-identical to the host decode);
+    otherwise the images are decoded on the host straight into their slots of a pinned uint8 batch
+    buffer.  One thread per usable host core (PIL and the library release the GIL while decoding), the
+    next two batches in flight while the caller uses the current one."""
     import concurrent.futures as cf
+    from . import jpeg
     from .distributed import usable_cpus
     workers = workers or usable_cpus()
+    paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
     with cf.ThreadPoolExecutor(workers) as ex:
         pin = torch.cuda.is_available()
 
-        def sub(c):  # one future per image, so a batch decodes on many threads at once
+        def host(c):
             h, w = sizes[c[0]]
             buf = torch.empty((len(c), 3, h, w), dtype=torch.uint8, pin_memory=pin)
-            return buf, [ex.submit(dataset.read_u8, i, buf[k]) for k, i in enumerate(c)]
+            return "host", buf, [ex.submit(dataset.read_u8, i, buf[k]) for k, i in enumerate(c)]
+
+        def sub(c):  # one future per image, so a batch decodes on many threads at once
+            if device_decode:
+                return "pk", None, [ex.submit(_packet_or_none, paths[i]) for i in c]
+            return host(c)
 
         fut = [sub(c) for c in chunks[:2]]
         for j, c in enumerate(chunks):
-            buf, fs = fut[j]
-            for f in fs:
-                f.result()
+            kind, buf, fs = fut[j]
+            res = [f.result() for f in fs]
+            if kind == "pk" and any(r is None for r in res):  # a file the device path does not take
+                kind, buf, fs = host(c)
+                res = [f.result() for f in fs]
             if j + 2 < len(chunks):
                 fut.append(sub(chunks[j + 2]))
             fut[j] = None
-            yield [dataset.img_names[i] for i in c], sizes[c[0]], buf
+            batch = jpeg.Packets(res, sizes[c[0]]) if kind == "pk" else buf
+            yield [dataset.img_names[i] for i in c], sizes[c[0]], batch
 
 
 def detect_rows(model, images, dataset="coco"):
@@ -163,7 +189,8 @@ def main(opts):
     shards = [dist_mod.batch_shard(chunks, r, world) for r in range(world)]
     shard_names = [[img_names[i] for c in sh for i in c] for sh in shards]
     my_names = shard_names[rank]
-    tagged = (((names, hw), buf) for names, hw, buf in _decoded_batches(dataset, shards[rank], sizes))
+    tagged = (((names, hw), buf) for names, hw, buf in
+              _decoded_batches(dataset, shards[rank], sizes, device_decode=getattr(opts, "decode", "gpu") == "gpu"))
     for (names, (h, w)), counts, boxes, scores, labels in model.run_batches(tagged, raw=True):
         for name, rows in zip(names, fmt.format_batch(boxes, scores, labels, counts, h, w, opts.dataset)):
             results[name] = rows
@@ -176,7 +203,7 @@ def main(opts):
 
 
 def getargs(argv=None):
-    """detect.py:109-121 (same positional/optional arguments and defaults) + --batch."""
+    """detect.py:109-121 (same positional/optional arguments and defaults) + --batch, --decode."""
     args = argparse.ArgumentParser()
     args.add_argument('img_dir', help="Directory that saves the image dataset for detection.")
     args.add_argument('save_dir', help="Directory to save the detection outputs.")
@@ -186,6 +213,9 @@ def getargs(argv=None):
     args.add_argument("--model-path", type=str, default="",
                       help="Location of the saved object detection model weights (torchvision state_dict keys).")
     args.add_argument("--batch", type=int, default=0, help="Images per engine call (0 = model default).")
+    args.add_argument("--decode", choices=("gpu", "host"), default="gpu",
+                      help="JPEG decode: entropy decode on the host + reconstruction on the GPU (byte-identical), "
+                           "or the whole decode on the host (PIL).")
     return args.parse_args(argv)
 
 

@@ -1,0 +1,112 @@
+"""Baseline-JPEG ingest on the device (csrc/jpeg.hip): torchvision.io.read_image(path, RGB) of
+detect.py:55-58 split into a host entropy decode (one image per host thread; ctypes releases the GIL)
+and a device reconstruction (dequantisation, islow IDCT, fancy upsampling, YCbCr -> RGB) that writes
+the uint8 [B,3,H,W] batch the detector plans read, byte-identical to libjpeg's default decode.
+
+    pk = packet(open(path, "rb").read())      # host: np.uint8 packet, or None if unsupported
+    dec = BatchDecoder(device)
+    dec.decode([pk0, pk1, ...], out_u8)        # device: out_u8 [B,3,H,W] uint8 (cuda tensor)
+
+JPEGs the device path does not handle (progressive, arithmetic-coded, CMYK / RGB JPEGs, unusual
+chroma samplings) come back as None from packet(); the caller decodes those files on the host.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+class Packets(list):
+    """The packets of one batch of equal-size images (a run_batches input: decoded on the device
+    straight into the plan's uint8 input)."""
+
+    def __init__(self, packets, hw):
+        super().__init__(packets)
+        self.hw = tuple(hw)
+
+
+def packet(data):
+    """Entropy-decode one JPEG file's bytes -> (packet np.uint8 array, (H, W)); (None, reason) when
+    the device path does not handle the file; raises EdgeDetError on corrupt data."""
+    L = ops.lib()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    hw = (ctypes.c_int32 * 2)()
+    # first call sizes the packet; the decode runs twice only when the guess is too small
+    cap = max(4096, 6 * buf.size + 65536)
+    out = np.empty(cap, np.uint8)
+    n = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, out.ctypes.data, cap, hw)
+    if n == 0:
+        return None, L.edgedet_last_error().decode()
+    if n < 0:
+        ops.check(int(n))
+    if n > cap:
+        out = np.empty(int(n), np.uint8)
+        m = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, out.ctypes.data, int(n), hw)
+        if m != n:
+            ops.check(int(m) if m < 0 else -1)
+    return out[:int(n)], (int(hw[0]), int(hw[1]))
+
+
+def plane_bytes(pk):
+    return int(ops.lib().edgedet_jpeg_plane_bytes(pk.ctypes.data))
+
+
+def reconstruct_host(pk, hw):
+    """The host checker of the device reconstruction (csrc/jpeg.hip reconstruct_host): [3,H,W] uint8."""
+    out = np.empty((3, hw[0], hw[1]), np.uint8)
+    ops.check(ops.lib().edgedet_jpeg_reconstruct_host(pk.ctypes.data, out.ctypes.data))
+    return out
+
+
+class BatchDecoder:
+    """Device reconstruction of batches of packets of one size into uint8 [B,3,H,W] device tensors.
+    Keeps a pinned staging buffer and a device copy of the packets and the plane scratch, grown as
+    needed; every call is asynchronous on the given stream (the caller keeps the packets' pinned
+    staging alive until the stream passes the upload: decode() records an event it waits on before
+    the staging is reused)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.stage = torch.empty(0, dtype=torch.uint8).pin_memory()
+        self.dev = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.planes = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.done = None
+
+    def decode(self, packets, out, stream=None):
+        B, C, H, W = out.shape
+        if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(packets) != B:
+            raise ValueError("decode: out must be a contiguous cuda uint8 [B,3,H,W] tensor, one packet per image")
+        # one upload: [offsets int64, padded to 256 B][packet 0][packet 1]... (each 256-B aligned)
+        head = (8 * B + 255) // 256 * 256
+        sizes = [int(p.size) for p in packets]
+        offs = np.zeros(B, np.int64)
+        offs[1:] = np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])[:-1]
+        offs += head
+        total = int(offs[-1] + sizes[-1])
+        blocks = [plane_bytes(p) // 64 for p in packets]
+        stride = (max(blocks) * 64 + 255) // 256 * 256
+        if self.done is not None:
+            self.done.synchronize()  # the previous batch's upload has left the staging buffer
+        if self.stage.numel() < total:
+            self.stage = torch.empty(total * 2, dtype=torch.uint8).pin_memory()
+        if self.dev.numel() < total:
+            self.dev = torch.empty(total * 2, dtype=torch.uint8, device=self.device)
+        if self.planes.numel() < B * stride:
+            self.planes = torch.empty(B * stride * 2, dtype=torch.uint8, device=self.device)
+        st = self.stage.numpy()
+        st[:8 * B] = offs.view(np.uint8)
+        for p, o in zip(packets, offs):
+            st[o:o + p.size] = p
+        s = stream or torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            self.dev[:total].copy_(self.stage[:total], non_blocking=True)
+            base = self.dev.data_ptr()
+            ops.check(ops.lib().edgedet_jpeg_decode_batch(ctypes.c_void_p(base), ctypes.c_void_p(base), B, H, W,
+                                                           max(blocks), ctypes.c_void_p(self.planes.data_ptr()),
+                                                           stride, ctypes.c_void_p(out.data_ptr()),
+                                                           ops.stream_handle(s)))
+            self.done = torch.cuda.Event()
+            self.done.record(s)
+        return out

@@ -164,7 +164,7 @@ class _Detector:
             B, H, W, u8 = key
             plan = self.plan(*key) if first else self.build_plan(*key).finalize()
             dt = torch.uint8 if u8 else torch.float32
-            return {"plan": plan, "stream": torch.cuda.Stream(self.device),
+            return {"plan": plan, "stream": torch.cuda.Stream(self.device), "jpeg": None,
                     "stage": torch.empty((B, 3, H, W), dtype=dt, pin_memory=True),
                     "count": torch.empty((B,), dtype=torch.int32, pin_memory=True),
                     "box": torch.empty(tuple(plan.out_box.shape), dtype=torch.float32, pin_memory=True),
@@ -189,9 +189,12 @@ class _Detector:
             return tag, [(box[j, :counts[j]].copy(), score[j, :counts[j]].copy(), label[j, :counts[j]].copy())
                          for j in range(B)]
 
+        from .jpeg import BatchDecoder, Packets
         for tag, imgs in batches:
             whole = imgs if torch.is_tensor(imgs) and imgs.dim() == 4 else None
-            if whole is not None:
+            if isinstance(imgs, Packets):  # JPEG packets: decoded on the device into the plan's input
+                shapes, dtypes, B = {imgs.hw}, {torch.uint8}, len(imgs)
+            elif whole is not None:
                 shapes, dtypes, B = {tuple(whole.shape[-2:])}, {whole.dtype}, whole.shape[0]
             else:
                 imgs = list(imgs)
@@ -215,7 +218,9 @@ class _Detector:
             plan, stream = sl["plan"], sl["stream"]
             stage = sl["stage"]
             sl["done"].synchronize()  # a slot left in flight by an abandoned earlier call
-            if whole is not None and whole.dtype in (torch.uint8, torch.float32) and whole.is_contiguous() and \
+            if isinstance(imgs, Packets):
+                src = None
+            elif whole is not None and whole.dtype in (torch.uint8, torch.float32) and whole.is_contiguous() and \
                     (whole.is_pinned() or whole.device == self.device):
                 # pinned host or already on the device: copied straight into the plan's input on the
                 # slot stream (no staging); held until the slot is collected (the copy is asynchronous)
@@ -231,7 +236,12 @@ class _Detector:
                 # instead of a host call per op, which kept the host, not the device, the bottleneck
                 plan.capture(stream)
             with torch.cuda.stream(stream):
-                plan.input.tensor().copy_(src, non_blocking=True)
+                if src is None:
+                    if sl["jpeg"] is None:
+                        sl["jpeg"] = BatchDecoder(self.device)
+                    sl["jpeg"].decode(imgs, plan.input.tensor(), stream)
+                else:
+                    plan.input.tensor().copy_(src, non_blocking=True)
                 plan.replay(stream)
                 sl["count"].copy_(plan.out_count.tensor(), non_blocking=True)
                 sl["box"].copy_(plan.out_box.tensor(), non_blocking=True)

@@ -35,7 +35,8 @@ def main(opts):
     dirs = {k: os.path.join(opts.work_dir, k) for k in ("weak", "strong", "reward")}
     for stage, model in (("weak", opts.weak), ("strong", opts.strong)):
         t0 = time.perf_counter()
-        detect.main(detect.getargs([opts.img_dir, dirs[stage], "--dataset", opts.dataset, "--model", model]))
+        detect.main(detect.getargs([opts.img_dir, dirs[stage], "--dataset", opts.dataset, "--model", model,
+                                    "--decode", getattr(opts, "decode", "gpu")]))
         _barrier()
         times[stage] = time.perf_counter() - t0
     t0 = time.perf_counter()
@@ -58,6 +59,7 @@ def getargs(argv=None):
     a.add_argument("--strong", default="faster_rcnn")
     a.add_argument("--num-ensemble", type=int, default=1000)
     a.add_argument("--seed", type=int, default=0)
+    a.add_argument("--decode", choices=("gpu", "host"), default="gpu", help="JPEG decode path of the detect stages")
     return a.parse_args(argv)
 
 

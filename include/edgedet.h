@@ -83,8 +83,10 @@ enum {
 int edgedet_plan_run(const edgedet_op* ops, int64_t n, void* stream);
 /* The lane-topology check alone (no device access): 0 or the error edgedet_plan_run would return. */
 int edgedet_plan_check(const edgedet_op* ops, int64_t n);
-/* Drop the side lanes (streams + events) the library keeps for `stream` (at most 16 sets are kept,
- * least recently used evicted; a set in use by a running call is destroyed when that call returns). */
+/* The library keeps side lanes (3 streams + events) per caller stream, at most 16 sets per device: a
+ * new caller stream beyond that takes over the least recently used set (sets are never destroyed:
+ * captured graphs refer to them).  edgedet_release_lanes marks `stream`'s set as the next to be taken
+ * over; edgedet_lane_sets returns the number of sets. */
 int edgedet_release_lanes(void* stream);
 int64_t edgedet_lane_sets(void);
 
@@ -353,6 +355,25 @@ int edgedet_map_eval(const int32_t* ent_img, const uint8_t* ent_flag, const int6
  */
 int edgedet_output_features(const double* rows, const int64_t* off, int64_t n_img, int32_t ncol, int32_t num_class,
                             int32_t k, double* out, void* stream);
+
+/* ------------------------------------------------------------------ image ingest (read_image) */
+/*
+ * torchvision.io.read_image(path, ImageReadMode.RGB) of detect.py:55-58 for baseline JPEGs, split
+ * host / device (csrc/jpeg.hip): edgedet_jpeg_packet entropy-decodes one file's bytes on the calling
+ * host thread into a packet (the nonzero coefficients of every 8x8 block + the quantisation tables);
+ * returns its size (written to out when cap suffices; hw = {H, W}), 0 for a JPEG it does not handle
+ * (progressive, arithmetic, CMYK/RGB, other samplings: decode that file on the host), < 0 on corrupt
+ * data.  edgedet_jpeg_decode_batch runs dequantisation + islow IDCT + fancy upsampling + YCbCr->RGB for
+ * B packets of one H x W already on the device (packets + offsets[b]) into out [B][3][H][W] uint8,
+ * byte-identical to libjpeg's default decode; planes: B * plane_stride bytes of scratch,
+ * plane_stride >= max_blocks * 64 = the largest edgedet_jpeg_plane_bytes of the batch.
+ * edgedet_jpeg_reconstruct_host is the same reconstruction on the host (test checker).
+ */
+int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* out, int64_t cap, int32_t* hw);
+int64_t edgedet_jpeg_plane_bytes(const void* host_packet);
+int edgedet_jpeg_decode_batch(const void* packets, const int64_t* offsets, int32_t B, int32_t H, int32_t W,
+                              int32_t max_blocks, void* planes, int64_t plane_stride, uint8_t* out, void* stream);
+int edgedet_jpeg_reconstruct_host(const void* host_packet, uint8_t* out);
 
 /* --------------------------------------------------------------------------------- misc */
 const char* edgedet_last_error(void);

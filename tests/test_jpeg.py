@@ -1,0 +1,89 @@
+"""Baseline-JPEG ingest (csrc/jpeg.hip; SURVEY §8(f) row 4, detect.py:55-58) on the CPU: the host
+entropy decoder's packets, reconstructed by the host checker that shares its integer arithmetic with the
+device kernels (csrc/jpeg_core.hpp), are byte-identical to the reference decoder's RGB image (PIL's
+libjpeg-turbo, the decode torchvision.io.read_image(..., RGB) performs with libjpeg), over qualities,
+chroma samplings, odd sizes, optimised Huffman tables, restart intervals and grayscale.  Unsupported
+files (progressive) are reported, not mis-decoded.  tests/test_gpu_jpeg.py checks the device path."""
+import io
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from edgeml_amd import jpeg, synthetic
+
+
+def _encode(img, **kw):
+    b = io.BytesIO()
+    img.save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _ref(data):
+    with Image.open(io.BytesIO(data)) as im:
+        return np.asarray(im.convert("RGB")).transpose(2, 0, 1)
+
+
+def _scene(h, w, seed):
+    return Image.fromarray(synthetic.make_scene(seed, h, w).transpose(1, 2, 0))
+
+
+CASES = [
+    dict(h=480, w=640, quality=75),                     # PIL default: 4:2:0
+    dict(h=427, w=640, quality=90, subsampling=0),      # 4:4:4
+    dict(h=375, w=500, quality=60, subsampling=1),      # 4:2:2
+    dict(h=333, w=501, quality=95),                     # odd width, 4:2:0
+    dict(h=101, w=67, quality=30),                      # MCU-ragged on both axes
+    dict(h=612, w=612, quality=85, optimize=True),      # optimised Huffman tables
+    dict(h=240, w=320, quality=75, restart_marker_blocks=7),
+    dict(h=241, w=333, quality=50, restart_marker_rows=1, subsampling=1),
+    dict(h=200, w=300, quality=100, subsampling=0),     # quality 100: large coefficients
+    dict(h=17, w=9, quality=75),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(str(c[k]) for k in ("h", "w")) + f"q{c['quality']}")
+def test_host_reconstruction_is_byte_exact(case):
+    c = dict(case)
+    h, w = c.pop("h"), c.pop("w")
+    data = _encode(_scene(h, w, h * 7 + w), **c)
+    pk, hw = jpeg.packet(data)
+    assert pk is not None, hw
+    assert hw == (h, w)
+    np.testing.assert_array_equal(jpeg.reconstruct_host(pk, hw), _ref(data))
+
+
+@pytest.mark.parametrize("h,w", [(480, 640), (99, 131)])
+def test_grayscale(h, w):
+    img = _scene(h, w, 3).convert("L")
+    data = _encode(img, quality=80)
+    pk, hw = jpeg.packet(data)
+    assert pk is not None
+    np.testing.assert_array_equal(jpeg.reconstruct_host(pk, hw), _ref(data))
+
+
+def test_noise_image_all_coefficients():
+    """Uniform noise: almost every coefficient nonzero (the dense extreme of the packet format)."""
+    rs = np.random.RandomState(0)
+    img = Image.fromarray(rs.randint(0, 256, (128, 192, 3), dtype=np.uint8))
+    data = _encode(img, quality=98, subsampling=0)
+    pk, hw = jpeg.packet(data)
+    np.testing.assert_array_equal(jpeg.reconstruct_host(pk, hw), _ref(data))
+
+
+def test_unsupported_and_corrupt():
+    data = _encode(_scene(120, 160, 1), quality=75, progressive=True)
+    pk, why = jpeg.packet(data)
+    assert pk is None and "progressive" in why
+    from edgeml_amd import ops
+    with pytest.raises(ops.EdgeDetError):
+        jpeg.packet(b"\x89PNG\r\n\x1a\n" + bytes(100))
+
+
+def test_packets_of_the_synthetic_dataset(tmp_path):
+    """The COCO-shaped synthetic JPEG set the pipeline benches use (synthetic.make_dataset)."""
+    names = synthetic.make_dataset(str(tmp_path), 6, seed=2, ext=".jpg")
+    for n in names:
+        data = (tmp_path / (n + ".jpg")).read_bytes()
+        pk, hw = jpeg.packet(data)
+        np.testing.assert_array_equal(jpeg.reconstruct_host(pk, hw), _ref(data))
