@@ -565,168 +565,173 @@ static int mbconv_front_launch(const DwParams& p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------ fused MBConv
-// A whole torchvision InvertedResidual without SqueezeExcitation (the SSDLite
-// backbone's high-resolution blocks 0.2 and 0.3): expand 1x1 (+ folded BN, act), depthwise KxK
-// stride S (+ folded BN, act), project 1x1 (+ folded BN), + the block input when S == 1 and
-// Cin == Cout.  Neither the 3-4x-wide expanded tensor nor the depthwise output reaches HBM: per
-// block (one image, an 8 x 8 output tile) the input halo ((8-1)*S + K)^2 x Cin is read once, and
-// the expanded channels are processed in chunks of 32 through LDS:
-//   expand   lane = one expanded channel of the chunk (its weight row in registers), a wave covers
-//            two halo pixels per step (broadcast LDS reads of the input row); halo pixels outside
-//            the image are zero (the depthwise pads the expanded tensor);
-//   depthwise taps in (kh, kw) order, as dw_group;
-//   project  partial sums over the chunk added in chunk order into registers (output pixel x
-//            output channel per thread), so the sum runs over the expanded channels in order.
-// All arithmetic is fp32 fmaf in the reference op order ((sum + bias) -> act; (sum + bias) + residual).
-// Measured 3.5-4.5x slower than the three separate ops on SSDLite blocks 0.2 / 0.3 (255 / 260 us
-// against 74 / 58 us per 16-image chain: at two blocks per CU each block's dependent phases leave its
-// LDS reads and VALU chains exposed, PMC: ~16 cycles per issued instruction), so the lowering keeps
-// the separate ops unless EDGEDET_MB_BLOCK=1.
-constexpr int MBF_T = 8, MBF_CC = 32, MBF_MAXCIN = 32, MBF_MAXCOUT = 32;
+// A whole torchvision InvertedResidual without SqueezeExcitation (SSDLite blocks
+// 0.2 / 0.3 at 160^2 / 80^2): expand 1x1 (+ folded BN, act), depthwise KxK stride S (+ folded BN, act),
+// project 1x1 (+ folded BN), + the block input when S == 1 and Cin == Cout.  Neither the 3-4x-wide
+// expanded tensor nor the depthwise output reaches HBM.  Block = one image, an 8 x 8 output tile,
+// 4 waves; the expanded channels are processed in chunks of 32 through LDS:
+//   expand   v_mfma_f32_32x32x2_f32 (exact fp32 products): [halo pixels, 32-row tiles over the waves]
+//            x [Cin] x [32 channels]; + bias, act; halo pixels outside the image are zero (the
+//            depthwise conv pads the expanded tensor with zeros);
+//   depthwise VALU from LDS, taps in (kh, kw) order, + bias, act;
+//   project  v_mfma_f32_32x32x2_f32: [64 output pixels] x [32 chunk channels] x [Cout], accumulated in
+//            registers over the chunks (waves own (pixel tile, Cout tile) pairs).
+// The round-2 form (expansion and projection on the VALU, one pixel x channel per thread) measured
+// 3.5-4.5x slower than the three separate ops; the matrix-core form keeps each phase to a few MFMAs
+// per wave.
+constexpr int MBF_T = 8, MBF_CC = 32;
+typedef float mbf_floatx16 __attribute__((ext_vector_type(16)));
 
-template <int K, int S, int CINB>
+template <int K, int S, int CINP>
 struct MbfGeom {
-    static constexpr int IH = (MBF_T - 1) * S + K, IP = IH * IH;
-    static constexpr int XS = CINB + 1, ES = MBF_CC + 1;
+    static constexpr int IH = (MBF_T - 1) * S + K, NPX = IH * IH, NPXP = (NPX + 31) / 32 * 32;
+    static constexpr int XS = CINP + 1;    // odd row pitch: conflict-free column reads
+    static constexpr int ES = MBF_CC + 1;  // expanded chunk row pitch
 };
 
-// CINB: the input-channel bound the block is compiled for (16 or 32; LDS rows and weight registers)
-template <int K, int S, int ACT, int CINB>
+// NCO: 32-wide Cout tiles (Cout <= 32 * NCO)
+template <int K, int S, int ACT, int CINP, int NCO>
 __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
-    using G = MbfGeom<K, S, CINB>;
-    constexpr int IH = G::IH, IP = G::IP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
-    constexpr int NOUT = (TT * MBF_MAXCOUT + 255) / 256;  // output items per thread
-    __shared__ float xs[IP * XS];  // input halo [pixel][Cin]
-    __shared__ float es[IP * ES];  // expanded chunk [halo pixel][32]
-    __shared__ float ds[TT * ES];  // depthwise chunk [output pixel][32]
-    __shared__ float w2s[MBF_MAXCOUT * ES];  // project weights of the chunk [co][32] (zero past Cexp)
-    const int tid = threadIdx.x, b = blockIdx.y;
+    using G = MbfGeom<K, S, CINP>;
+    constexpr int IH = G::IH, NPX = G::NPX, NPXP = G::NPXP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
+    constexpr int NPT = 2 * NCO;  // project tiles (2 pixel tiles x NCO Cout tiles), wave w owns w, w + 4
+    __shared__ float xs[NPXP * XS];        // input halo [pixel][Cin] (rows past NPX zero)
+    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]
+    __shared__ float ds[TT * ES];          // depthwise chunk [output pixel][32]
+    __shared__ float w1s[MBF_CC * XS];     // expand weights of the chunk [32][Cin]
+    __shared__ float w2s[32 * NCO * ES];   // project weights of the chunk [Cout pad][32]
+    __shared__ float wds[K * K * MBF_CC];  // depthwise taps of the chunk [tap][32]
+    __shared__ float b1s[MBF_CC], bds[MBF_CC];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, h = lane >> 5;
+    const int b = blockIdx.y;
     const int oh0 = (blockIdx.x / tiles_w) * MBF_T, ow0 = (blockIdx.x % tiles_w) * MBF_T;
     const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
     const int Cin = p.Cin, Cexp = p.Cexp, Cout = p.Cout;
     const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
-    // 1. input halo, all of a thread's loads in flight together
+    // 1. input halo (zero outside the image and past Cin), all loads of a thread in flight together
     {
-        constexpr int MAXN = (IP * CINB + 255) / 256;
-        const int n = IP * Cin;
-        float v[MAXN];
+        constexpr int N = NPXP * CINP, U = (N + 255) / 256;
+        float v[U];
 #pragma unroll
-        for (int r = 0; r < MAXN; ++r) {
+        for (int r = 0; r < U; ++r) {
             const int t = tid + 256 * r;
-            const int px = t / Cin, c = t - px * Cin;
+            const int px = t / CINP, c = t - px * CINP;
             const int ih = ih0 + px / IH, iw = iw0 + px % IH;
-            const bool in = t < n && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const bool in = t < N && px < NPX && c < Cin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             v[r] = in ? xb[((int64_t)ih * p.W + iw) * Cin + c] : 0.f;
         }
 #pragma unroll
-        for (int r = 0; r < MAXN; ++r) {
+        for (int r = 0; r < U; ++r) {
             const int t = tid + 256 * r;
-            if (t < n) {
-                const int px = t / Cin;
-                xs[px * XS + (t - px * Cin)] = v[r];
-            }
+            if (t < N) xs[(t / CINP) * XS + t % CINP] = v[r];
         }
     }
-    float acc[NOUT];
+    mbf_floatx16 acc[2];
 #pragma unroll
-    for (int r = 0; r < NOUT; ++r) acc[r] = 0.f;
-    const int cl = tid & (MBF_CC - 1), pg = tid >> 5;  // chunk channel, pixel group (8 groups)
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
     for (int c0 = 0; c0 < Cexp; c0 += MBF_CC) {
-        const int ce = c0 + cl;
-        const bool cok = ce < Cexp;
-        // 2. expand: channel ce of the halo pixels pg, pg + 8, ...
-        float w[CINB];
-#pragma unroll
-        for (int i = 0; i < CINB; ++i) w[i] = (cok && i < Cin) ? p.w1[(int64_t)ce * p.ld1 + i] : 0.f;
-        const float be = cok ? p.b1[ce] : 0.f;
-        constexpr int W2N = (MBF_MAXCOUT * MBF_CC + 255) / 256;
-        float w2v[W2N];
-#pragma unroll
-        for (int r = 0; r < W2N; ++r) {  // loads in flight across the expansion
-            const int t = tid + 256 * r, co = t / MBF_CC, j = t % MBF_CC;
-            w2v[r] = (co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
+        __syncthreads();  // xs written; the previous chunk's es / ds / weights consumed
+        // chunk weights: expand rows, project columns, depthwise taps, biases (zero past Cexp)
+        for (int t = tid; t < MBF_CC * CINP; t += 256) {
+            const int n = t / CINP, c = t - n * CINP;
+            w1s[n * XS + c] = (c0 + n < Cexp && c < Cin) ? p.w1[(int64_t)(c0 + n) * p.ld1 + c] : 0.f;
         }
-        __syncthreads();  // xs written / the previous chunk's es, ds and w2s consumed
-        for (int px = pg; px < IP; px += 8) {
-            const int ih = ih0 + px / IH, iw = iw0 + px % IH;
-            const float* xr = xs + px * XS;
-            float a = 0.f;
-#pragma unroll
-            for (int i = 0; i < CINB; ++i)
-                if (i < Cin) a = fmaf(w[i], xr[i], a);
-            const bool in = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            es[px * ES + cl] = in ? apply_act(a + be, ACT) : 0.f;
+        for (int t = tid; t < 32 * NCO * MBF_CC; t += 256) {
+            const int co = t / MBF_CC, j = t - co * MBF_CC;
+            w2s[co * ES + j] = (co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
         }
-#pragma unroll
-        for (int r = 0; r < W2N; ++r) {
-            const int t = tid + 256 * r;
-            w2s[(t / MBF_CC) * ES + t % MBF_CC] = w2v[r];
+        for (int t = tid; t < K * K * MBF_CC; t += 256) {
+            const int tap = t / MBF_CC, j = t - tap * MBF_CC;
+            wds[t] = c0 + j < Cexp ? p.wd[(int64_t)tap * Cexp + c0 + j] : 0.f;
+        }
+        if (tid < MBF_CC) {
+            b1s[tid] = c0 + tid < Cexp ? p.b1[c0 + tid] : 0.f;
+            bds[tid] = c0 + tid < Cexp ? p.bd[c0 + tid] : 0.f;
         }
         __syncthreads();
-        // 3. depthwise on the 8 x 8 output pixels (pixel groups of 8), taps in (kh, kw) order
+        // 2. expand: wave w takes 32-pixel row tiles w, w + 4, ...
+        for (int t = wid; t < NPXP / 32; t += 4) {
+            mbf_floatx16 e;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) e[r] = 0.f;
+            const float* ar = xs + (32 * t + l32) * XS + h;
+            const float* br = w1s + l32 * XS + h;
+#pragma unroll
+            for (int k = 0; k < CINP; k += 2) e = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], e, 0, 0, 0);
+            const float bias = b1s[l32];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int ih = ih0 + m / IH, iw = iw0 + m % IH;
+                const bool in = m < NPX && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+                es[m * ES + l32] = in ? apply_act(e[r] + bias, ACT) : 0.f;
+            }
+        }
+        __syncthreads();
+        // 3. depthwise: thread = (channel tid & 31, output pixels (tid >> 5) + 8 j)
         {
+            const int ch = tid & 31;
             float wt[K * K];
 #pragma unroll
-            for (int t = 0; t < K * K; ++t) wt[t] = cok ? p.wd[t * Cexp + ce] : 0.f;
-            const float bdv = cok ? p.bd[ce] : 0.f;
-            for (int op = pg; op < TT; op += 8) {
-                const int lh = op / MBF_T, lw = op % MBF_T;
-                const int oh = oh0 + lh;
+            for (int q = 0; q < K * K; ++q) wt[q] = wds[q * MBF_CC + ch];
+            const float bd = bds[ch];
+#pragma unroll
+            for (int j = 0; j < TT / 8; ++j) {
+                const int op = (tid >> 5) + 8 * j;
+                const int ly = op / MBF_T, lx = op % MBF_T;
                 float a = 0.f;
 #pragma unroll
-                for (int kh = 0; kh < K; ++kh) {
-                    if ((unsigned)(oh * S - p.pad + kh) >= (unsigned)p.H) continue;  // as dw_group: rows off the map
+                for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-                    for (int kw = 0; kw < K; ++kw) {
-                        const int iw = (ow0 + lw) * S - p.pad + kw;
-                        if ((unsigned)iw >= (unsigned)p.W) continue;
-                        a = fmaf(es[((lh * S + kh) * IH + lw * S + kw) * ES + cl], wt[kh * K + kw], a);
-                    }
-                }
-                ds[op * ES + cl] = apply_act(a + bdv, ACT);
+                    for (int kw = 0; kw < K; ++kw) a = fmaf(es[((ly * S + kh) * IH + lx * S + kw) * ES + ch], wt[kh * K + kw], a);
+                ds[op * ES + ch] = apply_act(a + bd, ACT);
             }
         }
         __syncthreads();
-        // 4. project: this chunk's partial sums, channel order (channels past Cexp: zero weight and
-        //    zero depthwise value, adding +0)
+        // 4. project: tile q of wave w = (pixel tile pt, Cout tile nt); K = the chunk's 32 channels
 #pragma unroll
-        for (int r = 0; r < NOUT; ++r) {
-            const int it = tid + 256 * r;
-            if (it < TT * Cout) {
-                const int op = it / Cout, co = it - op * Cout;
-                const float* dr = ds + op * ES;
-                const float* wr = w2s + co * ES;
-                float a = acc[r];
+        for (int q = 0; q < 2; ++q) {
+            const int tt = wid + 4 * q;
+            if (tt < NPT) {
+                const int pt = tt & 1, nt = tt >> 1;
+                const float* ar = ds + (32 * pt + l32) * ES + h;
+                const float* br = w2s + (32 * nt + l32) * ES + h;
 #pragma unroll
-                for (int j = 0; j < MBF_CC; ++j) a = fmaf(wr[j], dr[j], a);
-                acc[r] = a;
+                for (int k = 0; k < MBF_CC; k += 2) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc[q], 0, 0, 0);
             }
         }
     }
-    // 5. bias, residual, store
+    // 5. bias, residual, store (lane = output channel, registers = output pixels)
 #pragma unroll
-    for (int r = 0; r < NOUT; ++r) {
-        const int it = tid + 256 * r;
-        if (it < TT * Cout) {
-            const int op = it / Cout, co = it - op * Cout;
-            const int lh = op / MBF_T, lw = op % MBF_T, oh = oh0 + lh, ow = ow0 + lw;
-            if (oh < p.Ho && ow < p.Wo) {
-                float v = acc[r] + p.b2[co];
-                if (p.residual) v = v + xs[((lh + p.pad) * IH + lw + p.pad) * XS + co];  // S == 1: the input pixel
-                p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
-            }
+    for (int q = 0; q < 2; ++q) {
+        const int tt = wid + 4 * q;
+        if (tt >= NPT) continue;
+        const int pt = tt & 1, nt = tt >> 1;
+        const int co = 32 * nt + l32;
+        if (co >= Cout) continue;
+        const float bias = p.b2[co];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int op = 32 * pt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int ly = op / MBF_T, lx = op % MBF_T, oh = oh0 + ly, ow = ow0 + lx;
+            if (oh >= p.Ho || ow >= p.Wo) continue;
+            float v = acc[q][r] + bias;
+            if (p.residual) v = v + xs[((ly + p.pad) * IH + lx + p.pad) * XS + co];  // S == 1: the input pixel
+            p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
         }
     }
 }
 
-template <int K, int S, int CINB>
-static int mbconv_launch_ksc(const MbParams& p, hipStream_t s) {
+template <int K, int S, int CINP, int NCO>
+static int mbconv_launch_kc(const MbParams& p, hipStream_t s) {
     const int tiles_w = cdiv(p.Wo, MBF_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, MBF_T) * tiles_w), (unsigned)p.B);
     switch (p.act) {
-        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
-        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
-        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINB>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
         default: EDGEDET_REQUIRE(false, "mbconv: activation RE / R6 / HS");
     }
     EDGEDET_LAUNCH_CHECK();
@@ -735,13 +740,17 @@ static int mbconv_launch_ksc(const MbParams& p, hipStream_t s) {
 
 template <int K, int S>
 static int mbconv_launch_ks(const MbParams& p, hipStream_t s) {
-    return p.Cin <= 16 ? mbconv_launch_ksc<K, S, 16>(p, s) : mbconv_launch_ksc<K, S, 32>(p, s);
+    if (p.Cout <= 32) {
+        if (p.Cin <= 16) return mbconv_launch_kc<K, S, 16, 1>(p, s);
+        if (p.Cin <= 24) return mbconv_launch_kc<K, S, 24, 1>(p, s);
+        return mbconv_launch_kc<K, S, 32, 1>(p, s);
+    }
+    EDGEDET_REQUIRE(false, "mbconv: Cout <= 32");
 }
 
 int mbconv_launch(const MbParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w1 && p.b1 && p.wd && p.bd && p.w2 && p.b2 && p.y, "mbconv: null pointer");
-    EDGEDET_REQUIRE(p.Cin >= 1 && p.Cin <= MBF_MAXCIN && p.Cout >= 1 && p.Cout <= MBF_MAXCOUT && p.Cexp >= 1,
-                    "mbconv: Cin, Cout <= 32");
+    EDGEDET_REQUIRE(p.Cin >= 1 && p.Cin <= 32 && p.Cout >= 1 && p.Cout <= 32 && p.Cexp >= 1, "mbconv: Cin, Cout <= 32");
     EDGEDET_REQUIRE(p.ld1 >= p.Cin && p.ld2 >= p.Cexp, "mbconv: weight row strides");
     EDGEDET_REQUIRE(p.pad == (p.K - 1) / 2 && p.Ho == (p.H + 2 * p.pad - p.K) / p.stride + 1 &&
                     p.Wo == (p.W + 2 * p.pad - p.K) / p.stride + 1, "mbconv: 'same' padding shape");
