@@ -239,6 +239,14 @@ def op_work(op):
         return "retina_select", 0.0, 4.0 * i[0] * n * (i[3] + 4)
     if k == O.RETINA_CLASS_NMS:
         return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
+    if k == O.SSD_HEADS:  # per map: feature map in, depthwise + 1x1 weights, head outputs
+        B, nm, cols = i[0], i[1], i[4]
+        fl, by = 0.0, 0.0
+        for m in range(nm):
+            H, W, C = i[5 + 8 * m], i[6 + 8 * m], i[7 + 8 * m]
+            fl += 2.0 * B * H * W * C * (9 + 6 * cols)
+            by += 4.0 * (B * H * W * C + 10 * C + 6 * cols * (C + 1) + B * H * W * 6 * cols)
+        return "ssd_heads", fl, by
     if k in (O.FORK, O.JOIN, O.WAIT):
         return "lanes", 0.0, 0.0
     if k == O.MEMSET:  # zeroing the output of a split-K conv

@@ -54,6 +54,9 @@
 //                  i0..4 B,L,kin,K,kmax; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 //   WAIT           lane i0 waits for everything issued so far on lane i1 (both forked, or 0)
+//   SSD_HEADS      p0 weight blob base; p1..p5 feature maps [B,H,W,C]; p6 out [Btot,A,cols];
+//                  i0..4 B,nmaps,A,img0,cols; map m: i[5+8m..12+8m] = H,W,C,a0, float offsets from p0 of
+//                  the depthwise weights [9][C], depthwise bias, 1x1 weights [6*cols][C], 1x1 bias
 #include <cstdlib>
 #include <memory>
 #include <mutex>
@@ -175,6 +178,30 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
                 p.stdv[c] = o.f[3 + c];
             }
             return preprocess_launch(p, s);
+        }
+        case EDGEDET_OP_SSD_HEADS: {
+            SsdHeadsParams p{};
+            p.w = P<const float>(o, 0);
+            p.out = P<float>(o, 6);
+            p.B = (int)I[0];
+            p.nmaps = (int)I[1];
+            p.A = (int)I[2];
+            p.img0 = (int)I[3];
+            p.cols = (int)I[4];
+            EDGEDET_REQUIRE(p.nmaps >= 1 && p.nmaps <= 5, "ssd_heads: 1..5 maps");
+            for (int m = 0; m < p.nmaps; ++m) {
+                const int64_t* q = I + 5 + 8 * m;
+                p.feat[m] = P<const float>(o, 1 + m);
+                p.H[m] = (int)q[0];
+                p.W[m] = (int)q[1];
+                p.C[m] = (int)q[2];
+                p.a0[m] = (int)q[3];
+                p.dw_w[m] = q[4];
+                p.dw_b[m] = q[5];
+                p.cw[m] = q[6];
+                p.cb[m] = q[7];
+            }
+            return ssd_heads_launch(p, s);
         }
         case EDGEDET_OP_MBCONV: {
             MbParams p{};

@@ -762,6 +762,97 @@ int mbconv_launch(const MbParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(false, "mbconv: K in {3, 5}, stride in {1, 2}");
 }
 
+// ------------------------------------------------------------------------------ SSDLite small heads
+// SSDLiteHead on feature maps 1..5 (10x10 .. 1x1): per map and branch,
+// [dw3x3 + BN + ReLU6, 1x1 conv with bias], 10 layers x 2 ops that each launch a few thousand
+// threads for a few microseconds, as one launch per branch.  Block = (map, 64-wide output tile,
+// image): the map is processed in 32-channel chunks through LDS — the chunk of the feature map, its
+// depthwise output (taps in (kh, kw) order, out-of-map taps skipped, as the depthwise kernels), and the
+// chunk's 1x1 weights; thread (output n = lane, pixels wave + 4q) accumulates over the channels in
+// order (fp32 fma; the depthwise value is an LDS broadcast within the wave).  Outputs go to the
+// concatenated head tensor at (image, map anchor offset + pixel * 6 * cols + n), as the strided conv
+// epilogue stores them.
+constexpr int HD_CC = 32, HD_NT = 64, HD_MAXP = 100, HD_PQ = (HD_MAXP + 3) / 4;
+
+__global__ void __launch_bounds__(256) ssd_heads_kernel(SsdHeadsParams p) {
+    __shared__ float fs[HD_MAXP * (HD_CC + 1)];
+    __shared__ float ds[HD_MAXP * (HD_CC + 1)];
+    __shared__ float wc[HD_NT * (HD_CC + 1)];
+    __shared__ float wdw[9 * HD_CC], bdw[HD_CC];
+    const int nout = 6 * p.cols, ntiles = (nout + HD_NT - 1) / HD_NT;
+    const int m = blockIdx.x / ntiles, t = blockIdx.x - m * ntiles, b = blockIdx.y;
+    const int H = p.H[m], W = p.W[m], C = p.C[m], P = H * W;
+    const int n0 = t * HD_NT;
+    const float* f = p.feat[m] + (int64_t)b * P * C;
+    const float* wdw_g = p.w + p.dw_w[m];
+    const float* bdw_g = p.w + p.dw_b[m];
+    const float* wc_g = p.w + p.cw[m];
+    const int tid = threadIdx.x, n = tid & 63, g = tid >> 6;
+    float acc[HD_PQ];
+#pragma unroll
+    for (int q = 0; q < HD_PQ; ++q) acc[q] = 0.f;
+    for (int c0 = 0; c0 < C; c0 += HD_CC) {
+        __syncthreads();  // the previous chunk's fs / ds / wc consumed
+        for (int e = tid; e < P * HD_CC; e += 256) {
+            const int px = e / HD_CC, j = e - px * HD_CC;
+            fs[px * (HD_CC + 1) + j] = f[(int64_t)px * C + c0 + j];
+        }
+        for (int e = tid; e < 9 * HD_CC; e += 256) wdw[e] = wdw_g[(int64_t)(e / HD_CC) * C + c0 + e % HD_CC];
+        if (tid < HD_CC) bdw[tid] = bdw_g[c0 + tid];
+        for (int e = tid; e < HD_NT * HD_CC; e += 256) {
+            const int nn = e / HD_CC, j = e - nn * HD_CC;
+            wc[nn * (HD_CC + 1) + j] = n0 + nn < nout ? wc_g[(int64_t)(n0 + nn) * C + c0 + j] : 0.f;
+        }
+        __syncthreads();
+        for (int e = tid; e < P * HD_CC; e += 256) {
+            const int px = e / HD_CC, j = e - px * HD_CC;
+            const int y = px / W, x = px - y * W;
+            float a = 0.f;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const int yy = y - 1 + kh;
+                if ((unsigned)yy >= (unsigned)H) continue;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int xx = x - 1 + kw;
+                    if ((unsigned)xx >= (unsigned)W) continue;
+                    a = fmaf(fs[(yy * W + xx) * (HD_CC + 1) + j], wdw[(kh * 3 + kw) * HD_CC + j], a);
+                }
+            }
+            ds[px * (HD_CC + 1) + j] = apply_act(a + bdw[j], ACT_RELU6);
+        }
+        __syncthreads();
+        for (int j = 0; j < HD_CC; ++j) {
+            const float wv = wc[n * (HD_CC + 1) + j];
+#pragma unroll
+            for (int q = 0; q < HD_PQ; ++q) {
+                const int px = g + 4 * q;
+                if (px < P) acc[q] = fmaf(ds[px * (HD_CC + 1) + j], wv, acc[q]);
+            }
+        }
+    }
+    if (n0 + n >= nout) return;
+    const float bias = p.w[p.cb[m] + n0 + n];
+    float* out = p.out + ((int64_t)(p.img0 + b) * p.A + p.a0[m]) * p.cols;
+#pragma unroll
+    for (int q = 0; q < HD_PQ; ++q) {
+        const int px = g + 4 * q;
+        if (px < P) out[(int64_t)px * nout + n0 + n] = acc[q] + bias;
+    }
+}
+
+int ssd_heads_launch(const SsdHeadsParams& p, hipStream_t s) {
+    EDGEDET_REQUIRE(p.w && p.out && p.nmaps >= 1 && p.nmaps <= 5 && p.cols >= 1 && p.B >= 1, "ssd_heads: bad arguments");
+    for (int m = 0; m < p.nmaps; ++m) {
+        EDGEDET_REQUIRE(p.feat[m], "ssd_heads: null feature map");
+        EDGEDET_REQUIRE(p.H[m] * p.W[m] <= HD_MAXP && p.C[m] % HD_CC == 0, "ssd_heads: maps <= 100 pixels, C % 32 == 0");
+    }
+    const int ntiles = (6 * p.cols + HD_NT - 1) / HD_NT;
+    hipLaunchKernelGGL(ssd_heads_kernel, dim3((unsigned)(p.nmaps * ntiles), (unsigned)p.B), dim3(256), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
 // LDS bytes the fused front needs (0 = shape not supported); the plan uses it to decide fusion.
 extern "C" int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin) {
     if (K == 3 && stride == 1) return (int64_t)MbGeom<3, 1>::lds_bytes(Cin);

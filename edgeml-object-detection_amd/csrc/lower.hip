@@ -820,6 +820,21 @@ class SSDLite {
         int64_t off = 0;
         if (nch == 1) P.fork(3);
         int br = 0;
+        // maps 1..5 (10x10 and below) as one SSD_HEADS launch per branch (EDGEDET_SSD_HEADS=0: the
+        // separate depthwise + 1x1 pair per map and branch)
+        const bool group = !pack_only && env_int("EDGEDET_SSD_HEADS", 1) == 1;
+        OpRec grp[2];
+        for (int h = 0; h < 2; ++h) {
+            grp[h].kind = EDGEDET_OP_SSD_HEADS;
+            grp[h].name = std::string(h == 0 ? "head.classification_head" : "head.regression_head") + ".maps1-5" + sfx;
+            grp[h].p[0] = Plan::wref(WRef{0, 0, -1});
+            grp[h].p[6] = P.ref(h == 0 ? sh.cls : sh.reg);
+            grp[h].i[0] = B;
+            grp[h].i[1] = (int64_t)feats.size() - 1;
+            grp[h].i[2] = A;
+            grp[h].i[3] = img0;
+            grp[h].i[4] = h == 0 ? NC : 4;
+        }
         for (size_t i = 0; i < feats.size(); ++i) {
             const Cur& f = feats[i];
             for (int h = 0; h < 2; ++h) {
@@ -827,6 +842,17 @@ class SSDLite {
                 const int64_t cols = h == 0 ? NC : 4;
                 const int out = h == 0 ? sh.cls : sh.reg;
                 const std::string p = "head." + name + ".module_list." + std::to_string(i);
+                if (group && i >= 1) {
+                    ConvW wd = cbn(p + ".0", f.s[3], f.s[3], 3, true);
+                    ConvW w = pk_.conv_bias(p + ".1.weight", p + ".1.bias", 6 * cols, f.s[3], 1);
+                    if (w.Kpad != f.s[3]) throw std::runtime_error("ssd heads: C must be a multiple of 32");
+                    OpRec& g = grp[h];
+                    const int m = (int)i - 1;
+                    g.p[1 + m] = f.x;
+                    const int64_t v[8] = {f.s[1], f.s[2], f.s[3], off, wd.w.off, wd.b.off, w.w.off, w.b.off};
+                    for (int j = 0; j < 8; ++j) g.i[5 + 8 * m + j] = v[j];
+                    continue;
+                }
                 if (nch == 1) P.lane(br % 4);
                 ++br;
                 DwOut t = dw(f, p + ".0", 3, 1, A_R6, false);
@@ -846,6 +872,13 @@ class SSDLite {
                 conv_op(P, a);
             }
             off += f.s[1] * f.s[2] * 6;
+        }
+        if (group) {
+            for (int h = 0; h < 2; ++h) {
+                if (nch == 1) P.lane(br % 4);
+                ++br;
+                P.add(grp[h]);
+            }
         }
         if (nch == 1) P.join();
         if (pack_only) return;

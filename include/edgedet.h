@@ -69,7 +69,8 @@ enum {
     EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
     EDGEDET_OP_SSD_STEM = 21,     /* SSDLite features.0.0 + features.0.1 in one pass                  */
     EDGEDET_OP_MBCONV = 22,       /* InvertedResidual without SE: expand, depthwise, project, residual */
-    EDGEDET_OP_WAIT = 23          /* lane i[0] waits for everything issued so far on lane i[1]         */
+    EDGEDET_OP_WAIT = 23,         /* lane i[0] waits for everything issued so far on lane i[1]         */
+    EDGEDET_OP_SSD_HEADS = 24     /* SSDLite head branch (dw3x3 + 1x1) of feature maps 1..5, one launch  */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,

@@ -160,8 +160,12 @@ def test_ssd_plan_lowering():
     # two convs fewer each
     mb = kinds.count(ops.MBCONV)
     assert mb == (2 if os.environ.get("EDGEDET_MB_BLOCK") == "1" else 0)
-    assert n_dw == 15 + 4 + 12 - stem - mb
-    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + 12 - 2 * stem - 2 * mb
+    # the head branches of maps 1..5 as one SSD_HEADS op per branch (10 depthwise + 10 convs fewer)
+    grouped = os.environ.get("EDGEDET_SSD_HEADS") != "0"
+    assert kinds.count(ops.SSD_HEADS) == (2 if grouped else 0)
+    heads = 2 if grouped else 12
+    assert n_dw == 15 + 4 + heads - stem - mb
+    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + heads - 2 * stem - 2 * mb
     assert kinds.count(ops.SE_FC) == 8
     assert m.grids == [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
     for op in P.ops:
