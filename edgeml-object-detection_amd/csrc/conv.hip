@@ -833,13 +833,16 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 
 // bf16x6 with a 32-deep K stage: 256 x 128 block tile on 8 waves (4 x 2, 64 x 64 per wave), 48 MFMAs
 // per wave between barriers.  LDS rows are 32 bf16 (64 B) with the 16-B chunks XOR-swizzled by
-// row bits 2..3 (chunk' = chunk ^ ((row >> 2) & 3)): the four lane groups of a ds_read_b128 then hit
-// 16 distinct 16-B slots of the 256-B bank row (conflict-free), and the double-buffered image of the
+// row bit 3 (chunk' = chunk ^ ((row >> 2) & 2)).  The fragment reads are the 16x16x32 form (lane l:
+// row l & 15, chunk l >> 4), and the four ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,
+// 28-31}, and the same +32) then hit 16 distinct 16-B slots of the 256-B bank row (conflict-free; the
+// row bits 2..3 swizzle of the 32x32x16 form left them 2-way).  The double-buffered image of the
 // three A and three B planes fits 144 KiB (one block of 8 waves per CU, two waves per SIMD).
 constexpr int BK6B = 32;
 constexpr int X3Z = 32;  // leading zero elements of a pre-split scratch (16-B aligned planes follow)
 
-__device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int swz_key(int row) { return (row >> 2) & 2; }
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ swz_key(row)); }
 
 // XF: the input transform is active (SE scale / GN shift / ReLU); UT: Cin % 32 == 0, so every stage
 // lies inside one filter tap and the tap decomposition is wave-uniform (scalar) work.
@@ -956,7 +959,7 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
         if (GL && 16 * wid < BN) {
             // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
             // -> the 16-B slot l of the block); the swizzle is applied on the source address
-            const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 2) & 3);
+            const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ swz_key(row);
             const int n = n0 + row < p.Cout ? n0 + row : p.Cout - 1;
             const unsigned short* src = reinterpret_cast<const unsigned short*>(p.w3) + (int64_t)n * p.Kpad + k0 + 8 * lc;
 #pragma unroll
@@ -973,7 +976,7 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
 #pragma unroll
                 for (int j = 0; j < AJ; ++j) {
                     const int row = a_row0 + AST * j;
-                    const int lc = (lane & 3) ^ ((row >> 2) & 3);  // swizzle on the source address
+                    const int lc = (lane & 3) ^ swz_key(row);  // swizzle on the source address
                     const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
                     const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
 #pragma unroll

@@ -18,8 +18,6 @@
 //   SSD_STEM       p0 x NHWC4; p1 w0 [16][i5]; p2 b0; p3 wd [9][16]; p4 bd; p5 w1 [16][i6]; p6 b1; p7 y;
 //                  i0..4 B,H,W,Ho,Wo (SSDLite features.0.0 + features.0.1 fused)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
-//                  fused MBConv front when p5 != 0: p0 is the block input [B,H,W,i11 Cin], p5 the
-//                  1x1 expansion weight [C][i12 ld], p6 its bias, i13 its activation
 //                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16)
 //   MBCONV         InvertedResidual without SE in one kernel: p0 x; p1 expand w [Cexp][i12]; p2 b1;
 //                  p3 dw w [K*K][Cexp]; p4 bd; p5 project w [Cout][i13]; p6 b2; p7 y;
@@ -254,11 +252,6 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.pad = (int)I[8];
             p.act = (int)I[9];
             p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
-            p.w1 = P<const float>(o, 5);
-            p.b1 = P<const float>(o, 6);
-            p.Cin = (int)I[11];
-            p.w1_ld = (int)I[12];
-            p.act1 = (int)I[13];
             return dwconv_launch(p, s);
         }
         case EDGEDET_OP_CHANNEL_MEAN:

@@ -45,11 +45,6 @@ struct DwParams {
     float* part;     // optional SE squeeze partial sums [B][parts][C]
     int B, H, W, C, Ho, Wo, K, stride, pad, act;
     int parts;       // pixel splits of the squeeze (1..SE_PARTS)
-    // Fused MBConv front (w1 != null): x is the block input [B][H][W][Cin] and the depthwise input is
-    // the 1x1 expansion act1(w1 . x + b1), computed per tile in LDS and never written to HBM.
-    const float* w1;  // [C][w1_ld] packed 1x1 conv weight (folded BN), row c = expanded channel c
-    const float* b1;  // [C]
-    int Cin, w1_ld, act1;
 };
 
 // A whole InvertedResidual without SqueezeExcitation (csrc/layers.hip mbconv_kernel).

@@ -419,151 +419,6 @@ extern "C" int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W,
     return ssd_stem_launch(p, (hipStream_t)stream);
 }
 
-// ------------------------------------------------------------------------------ fused MBConv front
-// expand 1x1 (+BN, act1) -> depthwise KxK stride S (+BN, act2) for an InvertedResidual without SE
-// (torchvision mobilenetv3 InvertedResidual): the 6x-wide expanded tensor lives
-// only in LDS.  Block = one image, an 8 x 8 output tile and CC = 32 expanded channels (4 waves):
-//   1. the input halo tile ((8-1)*S + K)^2 x Cin is loaded into LDS (zeros outside the image), rows
-//      padded to Cin + 1 floats so the MFMA operand reads are conflict-free;
-//   2. expansion on the matrix cores: [halo pixels, padded to 32-row tiles] x [Cin] x [32 channels]
-//      with v_mfma_f32_32x32x2_f32 (exact fp32 products), + bias, act1; pixels outside the image are
-//      zero (the depthwise conv pads the expanded tensor);
-//   3. depthwise: thread (output pixel, channel quad), taps in (kh, kw) order as dw_group, + bias, act2.
-// Measured slower than the unfused pair on every SSDLite shape (tools/mb_bench.py, B=16: block 0.2
-// 69 vs 75 us, 0.7 61 vs 33 us): each block is three dependent latency phases (halo load, MFMA
-// expansion, depthwise) at two blocks per CU (70-100 KiB of LDS), and the halo load alone costs
-// half of the unfused pair.  So the lowering keeps the pair (EDGEDET_MBCONV_FUSE=1 selects this).
-constexpr int MB_TILE = 8, MB_CC = 32, MB_ES = MB_CC + 4;
-typedef float mb_floatx16 __attribute__((ext_vector_type(16)));
-
-template <int K, int S>
-struct MbGeom {
-    static constexpr int IH = (MB_TILE - 1) * S + K, IP = IH * IH, IPP = (IP + 31) / 32 * 32;
-    static size_t lds_bytes(int cin) {
-        return sizeof(float) * ((size_t)IPP * (cin + 4) + (size_t)MB_CC * (cin + 4) + (size_t)IPP * MB_ES);
-    }
-};
-
-template <int K, int S, int ACT1>
-__global__ void __launch_bounds__(256) mbconv_front_kernel(DwParams p, int tiles_w, int nchunk) {
-    using G = MbGeom<K, S>;
-    constexpr int IH = G::IH, IP = G::IP, IPP = G::IPP;
-    extern __shared__ __attribute__((aligned(16))) float mb_sm[];
-    const int Cin = p.Cin, XS = Cin + 4;
-    float* xs = mb_sm;            // [IPP][Cin + 4]: 16-B rows, 16 consecutive rows on distinct banks
-    float* ws = xs + IPP * XS;    // [MB_CC][Cin + 4]
-    float* es = ws + MB_CC * XS;  // [IPP][MB_ES]
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int b = blockIdx.y;
-    const int chunk = blockIdx.x % nchunk, tile = blockIdx.x / nchunk;
-    const int oh0 = (tile / tiles_w) * MB_TILE, ow0 = (tile % tiles_w) * MB_TILE;
-    const int c0 = chunk * MB_CC;
-    const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
-
-    // 1. input halo and the chunk's expansion weights
-    const int q4 = Cin >> 2;
-    const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
-    for (int v = tid; v < IPP * q4; v += 256) {
-        const int pp = v / q4, q = v - pp * q4;
-        const int ih = ih0 + pp / IH, iw = iw0 + pp % IH;
-        f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (pp < IP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-            xv = *reinterpret_cast<const f32x4*>(xb + ((int64_t)ih * p.W + iw) * Cin + 4 * q);
-        *reinterpret_cast<f32x4*>(xs + pp * XS + 4 * q) = xv;
-    }
-    for (int v = tid; v < MB_CC * q4; v += 256) {
-        const int n = v / q4, q = v - n * q4;
-        f32x4 wv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (c0 + n < p.C) wv = *reinterpret_cast<const f32x4*>(p.w1 + (int64_t)(c0 + n) * p.w1_ld + 4 * q);
-        *reinterpret_cast<f32x4*>(ws + n * XS + 4 * q) = wv;
-    }
-    __syncthreads();
-
-    // 2. expansion: wave w takes 32-pixel row tiles w, w + 4, ...; lane half h supplies the channels
-    //    [h * Cin/2, (h+1) * Cin/2) in order, four MFMA steps per ds_read_b128 of each operand
-    {
-        const int l32 = lane & 31, h = lane >> 5;
-        const int n = l32, c = c0 + n;
-        const int kh = Cin >> 1;  // Cin % 8 == 0
-        const float bias1 = c < p.C ? p.b1[c] : 0.f;
-        const float* br = ws + n * XS + h * kh;
-        for (int t = wid; t < IPP / 32; t += 4) {
-            mb_floatx16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-            const float* ar = xs + (32 * t + l32) * XS + h * kh;
-            for (int k = 0; k < kh; k += 4) {
-                const f32x4 av = *reinterpret_cast<const f32x4*>(ar + k);
-                const f32x4 bv = *reinterpret_cast<const f32x4*>(br + k);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int ih = ih0 + m / IH, iw = iw0 + m % IH;
-                const bool in = m < IP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && c < p.C;
-                es[m * MB_ES + n] = in ? apply_act(acc[r] + bias1, ACT1) : 0.f;  // ACT1 constant: no branch
-            }
-        }
-    }
-    __syncthreads();
-
-    // 3. depthwise: 64 pixels x 8 channel quads, two per thread
-    for (int it = tid; it < MB_TILE * MB_TILE * (MB_CC / 4); it += 256) {
-        const int o = it >> 3, q = it & 7;
-        const int oh = oh0 + o / MB_TILE, ow = ow0 + o % MB_TILE;
-        const int c = c0 + 4 * q;
-        if (oh >= p.Ho || ow >= p.Wo || c >= p.C) continue;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int lh0 = (o / MB_TILE) * S, lw0 = (o % MB_TILE) * S;
-#pragma unroll
-        for (int kh = 0; kh < K; ++kh) {
-            if ((unsigned)(ih0 + lh0 + kh) >= (unsigned)p.H) continue;  // dw_group skips rows outside the map
-#pragma unroll
-            for (int kw = 0; kw < K; ++kw) {
-                const f32x4 xv = *reinterpret_cast<const f32x4*>(es + ((lh0 + kh) * IH + lw0 + kw) * MB_ES + 4 * q);
-                const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * K + kw) * p.C + c);
-                acc.x = fmaf(xv.x, wv.x, acc.x);
-                acc.y = fmaf(xv.y, wv.y, acc.y);
-                acc.z = fmaf(xv.z, wv.z, acc.z);
-                acc.w = fmaf(xv.w, wv.w, acc.w);
-            }
-        }
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
-        f32x4 v;
-        v.x = apply_act(acc.x + bv.x, p.act);
-        v.y = apply_act(acc.y + bv.y, p.act);
-        v.z = apply_act(acc.z + bv.z, p.act);
-        v.w = apply_act(acc.w + bv.w, p.act);
-        *reinterpret_cast<f32x4*>(p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow) * p.C + c) = v;
-    }
-}
-
-template <int K, int S>
-static int mbconv_front_launch(const DwParams& p, hipStream_t s) {
-    const size_t lds = MbGeom<K, S>::lds_bytes(p.Cin);
-    EDGEDET_REQUIRE(lds <= 160 * 1024, "mbconv_front: input halo tile too large for LDS");
-    const int tiles_w = cdiv(p.Wo, MB_TILE), tiles = cdiv(p.Ho, MB_TILE) * tiles_w, nchunk = cdiv(p.C, MB_CC);
-    EDGEDET_REQUIRE(p.act1 >= 0 && p.act1 <= 3, "mbconv_front: expansion activation none / RE / R6 / HS");
-    static bool attr = false;
-    auto k = p.act1 == 0 ? mbconv_front_kernel<K, S, 0>
-                         : p.act1 == 1 ? mbconv_front_kernel<K, S, 1>
-                                       : p.act1 == 2 ? mbconv_front_kernel<K, S, 2> : mbconv_front_kernel<K, S, 3>;
-    if (!attr) {
-        for (auto f : {mbconv_front_kernel<K, S, 0>, mbconv_front_kernel<K, S, 1>, mbconv_front_kernel<K, S, 2>,
-                       mbconv_front_kernel<K, S, 3>})
-            EDGEDET_CHECK_HIP(
-                hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
-    hipLaunchKernelGGL(k, dim3((unsigned)(tiles * nchunk), (unsigned)p.B), dim3(256), lds, s, p, tiles_w, nchunk);
-    EDGEDET_LAUNCH_CHECK();
-    return 0;
-}
-
 // ------------------------------------------------------------------------------ fused MBConv
 // A whole torchvision InvertedResidual without SqueezeExcitation (SSDLite blocks
 // 0.2 / 0.3 at 160^2 / 80^2): expand 1x1 (+ folded BN, act), depthwise KxK stride S (+ folded BN, act),
@@ -589,25 +444,82 @@ struct MbfGeom {
     static constexpr int ES = MBF_CC + 1;  // expanded chunk row pitch
 };
 
-// NCO: 32-wide Cout tiles (Cout <= 32 * NCO)
+// NCO: 32-wide Cout tiles (Cout <= 32 * NCO; the launcher instantiates NCO = 1).  A chunk's weights
+// (expand rows, project columns, depthwise taps, biases) are loaded into registers one chunk ahead, all
+// loads of a thread issued together, and stored to LDS at the chunk boundary; the projection's two
+// 32-pixel tiles are split over the four waves by K half (waves 2, 3 take channels 16..31 of each
+// chunk), and the two halves are added once at the end (fixed order).
 template <int K, int S, int ACT, int CINP, int NCO>
 __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
+    static_assert(NCO == 1, "mbconv: the K-split projection is laid out for one Cout tile");
     using G = MbfGeom<K, S, CINP>;
     constexpr int IH = G::IH, NPX = G::NPX, NPXP = G::NPXP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
-    constexpr int NPT = 2 * NCO;  // project tiles (2 pixel tiles x NCO Cout tiles), wave w owns w, w + 4
     __shared__ float xs[NPXP * XS];        // input halo [pixel][Cin] (rows past NPX zero)
-    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]
+    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]; at the end the K-half partials
     __shared__ float ds[TT * ES];          // depthwise chunk [output pixel][32]
     __shared__ float w1s[MBF_CC * XS];     // expand weights of the chunk [32][Cin]
     __shared__ float w2s[32 * NCO * ES];   // project weights of the chunk [Cout pad][32]
     __shared__ float wds[K * K * MBF_CC];  // depthwise taps of the chunk [tap][32]
     __shared__ float b1s[MBF_CC], bds[MBF_CC];
+    static_assert(2 * 64 * 16 <= NPXP * ES, "K-half partials fit the expanded-chunk buffer");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, h = lane >> 5;
     const int b = blockIdx.y;
     const int oh0 = (blockIdx.x / tiles_w) * MBF_T, ow0 = (blockIdx.x % tiles_w) * MBF_T;
     const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
     const int Cin = p.Cin, Cexp = p.Cexp, Cout = p.Cout;
     const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
+    // chunk operands in registers (zero past Cexp / Cin / Cout)
+    constexpr int N1 = MBF_CC * CINP, N2 = 32 * NCO * MBF_CC, ND = K * K * MBF_CC + 2 * MBF_CC;
+    constexpr int U1 = (N1 + 255) / 256, U2 = (N2 + 255) / 256, UD = (ND + 255) / 256;
+    float r1[U1], r2[U2], rd[UD];
+    auto load_chunk = [&](int c0) {
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            const int t = tid + 256 * u, n = t / CINP, c = t - n * CINP;
+            r1[u] = (t < N1 && c0 + n < Cexp && c < Cin) ? p.w1[(int64_t)(c0 + n) * p.ld1 + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            const int t = tid + 256 * u, co = t / MBF_CC, j = t - co * MBF_CC;
+            r2[u] = (t < N2 && co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int t = tid + 256 * u;
+            float v = 0.f;
+            if (t < K * K * MBF_CC) {
+                const int tap = t / MBF_CC, j = t - tap * MBF_CC;
+                v = c0 + j < Cexp ? p.wd[(int64_t)tap * Cexp + c0 + j] : 0.f;
+            } else if (t < K * K * MBF_CC + MBF_CC) {
+                const int j = t - K * K * MBF_CC;
+                v = c0 + j < Cexp ? p.b1[c0 + j] : 0.f;
+            } else if (t < ND) {
+                const int j = t - K * K * MBF_CC - MBF_CC;
+                v = c0 + j < Cexp ? p.bd[c0 + j] : 0.f;
+            }
+            rd[u] = v;
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            const int t = tid + 256 * u, n = t / CINP, c = t - n * CINP;
+            if (t < N1) w1s[n * XS + c] = r1[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            const int t = tid + 256 * u, co = t / MBF_CC, j = t - co * MBF_CC;
+            if (t < N2) w2s[co * ES + j] = r2[u];
+        }
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int t = tid + 256 * u;
+            if (t < K * K * MBF_CC) wds[t] = rd[u];
+            else if (t < K * K * MBF_CC + MBF_CC) b1s[t - K * K * MBF_CC] = rd[u];
+            else if (t < ND) bds[t - K * K * MBF_CC - MBF_CC] = rd[u];
+        }
+    };
+    load_chunk(0);
     // 1. input halo (zero outside the image and past Cin), all loads of a thread in flight together
     {
         constexpr int N = NPXP * CINP, U = (N + 255) / 256;
@@ -626,30 +538,14 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
             if (t < N) xs[(t / CINP) * XS + t % CINP] = v[r];
         }
     }
-    mbf_floatx16 acc[2];
+    mbf_floatx16 acc;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int pt = wid & 1, kh0 = 16 * (wid >> 1);  // projection: pixel tile, K half of the chunk
     for (int c0 = 0; c0 < Cexp; c0 += MBF_CC) {
         __syncthreads();  // xs written; the previous chunk's es / ds / weights consumed
-        // chunk weights: expand rows, project columns, depthwise taps, biases (zero past Cexp)
-        for (int t = tid; t < MBF_CC * CINP; t += 256) {
-            const int n = t / CINP, c = t - n * CINP;
-            w1s[n * XS + c] = (c0 + n < Cexp && c < Cin) ? p.w1[(int64_t)(c0 + n) * p.ld1 + c] : 0.f;
-        }
-        for (int t = tid; t < 32 * NCO * MBF_CC; t += 256) {
-            const int co = t / MBF_CC, j = t - co * MBF_CC;
-            w2s[co * ES + j] = (co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
-        }
-        for (int t = tid; t < K * K * MBF_CC; t += 256) {
-            const int tap = t / MBF_CC, j = t - tap * MBF_CC;
-            wds[t] = c0 + j < Cexp ? p.wd[(int64_t)tap * Cexp + c0 + j] : 0.f;
-        }
-        if (tid < MBF_CC) {
-            b1s[tid] = c0 + tid < Cexp ? p.b1[c0 + tid] : 0.f;
-            bds[tid] = c0 + tid < Cexp ? p.bd[c0 + tid] : 0.f;
-        }
+        store_chunk();
+        if (c0 + MBF_CC < Cexp) load_chunk(c0 + MBF_CC);  // in flight under this chunk's three phases
         __syncthreads();
         // 2. expand: wave w takes 32-pixel row tiles w, w + 4, ...
         for (int t = wid; t < NPXP / 32; t += 4) {
@@ -690,37 +586,33 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
             }
         }
         __syncthreads();
-        // 4. project: tile q of wave w = (pixel tile pt, Cout tile nt); K = the chunk's 32 channels
+        // 4. project: wave w = (pixel tile w & 1, K half w >> 1) over the Cout tile
+        {
+            const float* ar = ds + (32 * pt + l32) * ES + kh0 + h;
+            const float* br = w2s + l32 * ES + kh0 + h;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int tt = wid + 4 * q;
-            if (tt < NPT) {
-                const int pt = tt & 1, nt = tt >> 1;
-                const float* ar = ds + (32 * pt + l32) * ES + h;
-                const float* br = w2s + (32 * nt + l32) * ES + h;
-#pragma unroll
-                for (int k = 0; k < MBF_CC; k += 2) acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc[q], 0, 0, 0);
-            }
+            for (int k = 0; k < MBF_CC / 2; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc, 0, 0, 0);
         }
     }
-    // 5. bias, residual, store (lane = output channel, registers = output pixels)
+    // 5. the upper K half's partials through LDS (es is free: every wave is past the last depthwise)
+    if (wid >= 2) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int tt = wid + 4 * q;
-        if (tt >= NPT) continue;
-        const int pt = tt & 1, nt = tt >> 1;
-        const int co = 32 * nt + l32;
-        if (co >= Cout) continue;
-        const float bias = p.b2[co];
+        for (int r = 0; r < 16; ++r) es[((wid - 2) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wid >= 2) return;
+    // 6. bias, residual, store (lane = output channel, registers = output pixels)
+    const int co = l32;
+    if (co >= Cout) return;
+    const float bias = p.b2[co];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int op = 32 * pt + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int ly = op / MBF_T, lx = op % MBF_T, oh = oh0 + ly, ow = ow0 + lx;
-            if (oh >= p.Ho || ow >= p.Wo) continue;
-            float v = acc[q][r] + bias;
-            if (p.residual) v = v + xs[((ly + p.pad) * IH + lx + p.pad) * XS + co];  // S == 1: the input pixel
-            p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
-        }
+    for (int r = 0; r < 16; ++r) {
+        const int op = 32 * pt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int ly = op / MBF_T, lx = op % MBF_T, oh = oh0 + ly, ow = ow0 + lx;
+        if (oh >= p.Ho || ow >= p.Wo) continue;
+        float v = (acc[r] + es[(wid * 16 + r) * 64 + lane]) + bias;
+        if (p.residual) v = v + xs[((ly + p.pad) * IH + lx + p.pad) * XS + co];  // S == 1: the input pixel
+        p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
     }
 }
 
@@ -768,17 +660,22 @@ int mbconv_launch(const MbParams& p, hipStream_t s) {
 // threads for a few microseconds, as one launch per branch.  Block = (map, 64-wide output tile,
 // image): the map is processed in 32-channel chunks through LDS — the chunk of the feature map, its
 // depthwise output (taps in (kh, kw) order, out-of-map taps skipped, as the depthwise kernels), and the
-// chunk's 1x1 weights; thread (output n = lane, pixels wave + 4q) accumulates over the channels in
-// order (fp32 fma; the depthwise value is an LDS broadcast within the wave).  Outputs go to the
-// concatenated head tensor at (image, map anchor offset + pixel * 6 * cols + n), as the strided conv
-// epilogue stores them.
-constexpr int HD_CC = 32, HD_NT = 64, HD_MAXP = 100, HD_PQ = (HD_MAXP + 3) / 4;
+// chunk's 1x1 weights; each output accumulates over the channels in order (fp32 fma).  Every global load of a
+// chunk is issued at once into registers one chunk ahead (a strided load-then-store loop would wait
+// out one memory round trip per element).  Outputs go to the concatenated head tensor at (image, map
+// anchor offset + pixel * 6 * cols + n), as the strided conv epilogue stores them.
+// 1x1 register block: thread (nl = tid & 15, pg = tid >> 4) owns outputs n0 + nl + 16k (k < 4) at
+// pixels pg + 16q (q < 7), so one LDS read of a depthwise value feeds four FMAs.
+constexpr int HD_CC = 32, HD_NT = 64, HD_MAXP = 100, HD_NO = HD_NT / 16, HD_PQ = (HD_MAXP + 15) / 16;
+constexpr int HD_FQ = (HD_MAXP * HD_CC / 4 + 255) / 256;  // feature f32x4 per thread per chunk
+constexpr int HD_WQ = HD_NT * HD_CC / 256;                // 1x1 weights per thread per chunk
+constexpr int HD_DQ = (9 * HD_CC + HD_CC + 255) / 256;    // depthwise taps + bias per thread per chunk
 
 __global__ void __launch_bounds__(256) ssd_heads_kernel(SsdHeadsParams p) {
     __shared__ float fs[HD_MAXP * (HD_CC + 1)];
     __shared__ float ds[HD_MAXP * (HD_CC + 1)];
     __shared__ float wc[HD_NT * (HD_CC + 1)];
-    __shared__ float wdw[9 * HD_CC], bdw[HD_CC];
+    __shared__ float wdw[10 * HD_CC];  // 9 taps, then the bias
     const int nout = 6 * p.cols, ntiles = (nout + HD_NT - 1) / HD_NT;
     const int m = blockIdx.x / ntiles, t = blockIdx.x - m * ntiles, b = blockIdx.y;
     const int H = p.H[m], W = p.W[m], C = p.C[m], P = H * W;
@@ -787,22 +684,58 @@ __global__ void __launch_bounds__(256) ssd_heads_kernel(SsdHeadsParams p) {
     const float* wdw_g = p.w + p.dw_w[m];
     const float* bdw_g = p.w + p.dw_b[m];
     const float* wc_g = p.w + p.cw[m];
-    const int tid = threadIdx.x, n = tid & 63, g = tid >> 6;
-    float acc[HD_PQ];
+    const int tid = threadIdx.x, nl = tid & 15, pg = tid >> 4;
+    f32x4 fr[HD_FQ];
+    float wr[HD_WQ], dr[HD_DQ];
+    auto load = [&](int c0) {
 #pragma unroll
-    for (int q = 0; q < HD_PQ; ++q) acc[q] = 0.f;
+        for (int u = 0; u < HD_FQ; ++u) {
+            const int e = tid + 256 * u, px = e >> 3;  // 8 quads per pixel
+            fr[u] = px < P ? *reinterpret_cast<const f32x4*>(f + (int64_t)px * C + c0 + 4 * (e & 7))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < HD_WQ; ++u) {
+            const int e = tid + 256 * u, nn = e / HD_CC;
+            wr[u] = n0 + nn < nout ? wc_g[(int64_t)(n0 + nn) * C + c0 + (e % HD_CC)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < HD_DQ; ++u) {
+            const int e = tid + 256 * u;
+            dr[u] = e < 9 * HD_CC ? wdw_g[(int64_t)(e / HD_CC) * C + c0 + e % HD_CC]
+                                  : (e < 10 * HD_CC ? bdw_g[c0 + e - 9 * HD_CC] : 0.f);
+        }
+    };
+    float acc[HD_NO][HD_PQ];
+#pragma unroll
+    for (int k = 0; k < HD_NO; ++k)
+#pragma unroll
+        for (int q = 0; q < HD_PQ; ++q) acc[k][q] = 0.f;
+    load(0);
     for (int c0 = 0; c0 < C; c0 += HD_CC) {
         __syncthreads();  // the previous chunk's fs / ds / wc consumed
-        for (int e = tid; e < P * HD_CC; e += 256) {
-            const int px = e / HD_CC, j = e - px * HD_CC;
-            fs[px * (HD_CC + 1) + j] = f[(int64_t)px * C + c0 + j];
+#pragma unroll
+        for (int u = 0; u < HD_FQ; ++u) {
+            const int e = tid + 256 * u, px = e >> 3, j = 4 * (e & 7);
+            if (px < P) {
+                float* d = fs + px * (HD_CC + 1) + j;
+                d[0] = fr[u].x;
+                d[1] = fr[u].y;
+                d[2] = fr[u].z;
+                d[3] = fr[u].w;
+            }
         }
-        for (int e = tid; e < 9 * HD_CC; e += 256) wdw[e] = wdw_g[(int64_t)(e / HD_CC) * C + c0 + e % HD_CC];
-        if (tid < HD_CC) bdw[tid] = bdw_g[c0 + tid];
-        for (int e = tid; e < HD_NT * HD_CC; e += 256) {
-            const int nn = e / HD_CC, j = e - nn * HD_CC;
-            wc[nn * (HD_CC + 1) + j] = n0 + nn < nout ? wc_g[(int64_t)(n0 + nn) * C + c0 + j] : 0.f;
+#pragma unroll
+        for (int u = 0; u < HD_WQ; ++u) {
+            const int e = tid + 256 * u;
+            wc[(e / HD_CC) * (HD_CC + 1) + e % HD_CC] = wr[u];
         }
+#pragma unroll
+        for (int u = 0; u < HD_DQ; ++u) {
+            const int e = tid + 256 * u;
+            if (e < 10 * HD_CC) wdw[e] = dr[u];
+        }
+        if (c0 + HD_CC < C) load(c0 + HD_CC);  // in flight under this chunk's compute
         __syncthreads();
         for (int e = tid; e < P * HD_CC; e += 256) {
             const int px = e / HD_CC, j = e - px * HD_CC;
@@ -819,25 +752,35 @@ __global__ void __launch_bounds__(256) ssd_heads_kernel(SsdHeadsParams p) {
                     a = fmaf(fs[(yy * W + xx) * (HD_CC + 1) + j], wdw[(kh * 3 + kw) * HD_CC + j], a);
                 }
             }
-            ds[px * (HD_CC + 1) + j] = apply_act(a + bdw[j], ACT_RELU6);
+            ds[px * (HD_CC + 1) + j] = apply_act(a + wdw[9 * HD_CC + j], ACT_RELU6);
         }
         __syncthreads();
         for (int j = 0; j < HD_CC; ++j) {
-            const float wv = wc[n * (HD_CC + 1) + j];
+            float wv[HD_NO];
+#pragma unroll
+            for (int k = 0; k < HD_NO; ++k) wv[k] = wc[(nl + 16 * k) * (HD_CC + 1) + j];
 #pragma unroll
             for (int q = 0; q < HD_PQ; ++q) {
-                const int px = g + 4 * q;
-                if (px < P) acc[q] = fmaf(ds[px * (HD_CC + 1) + j], wv, acc[q]);
+                const int px = pg + 16 * q;
+                if (px < P) {
+                    const float d = ds[px * (HD_CC + 1) + j];
+#pragma unroll
+                    for (int k = 0; k < HD_NO; ++k) acc[k][q] = fmaf(d, wv[k], acc[k][q]);
+                }
             }
         }
     }
-    if (n0 + n >= nout) return;
-    const float bias = p.w[p.cb[m] + n0 + n];
     float* out = p.out + ((int64_t)(p.img0 + b) * p.A + p.a0[m]) * p.cols;
 #pragma unroll
-    for (int q = 0; q < HD_PQ; ++q) {
-        const int px = g + 4 * q;
-        if (px < P) out[(int64_t)px * nout + n0 + n] = acc[q] + bias;
+    for (int k = 0; k < HD_NO; ++k) {
+        const int nn = n0 + nl + 16 * k;
+        if (nn >= nout) continue;
+        const float bias = p.w[p.cb[m] + nn];
+#pragma unroll
+        for (int q = 0; q < HD_PQ; ++q) {
+            const int px = pg + 16 * q;
+            if (px < P) out[(int64_t)px * nout + nn] = acc[k][q] + bias;
+        }
     }
 }
 
@@ -846,6 +789,7 @@ int ssd_heads_launch(const SsdHeadsParams& p, hipStream_t s) {
     for (int m = 0; m < p.nmaps; ++m) {
         EDGEDET_REQUIRE(p.feat[m], "ssd_heads: null feature map");
         EDGEDET_REQUIRE(p.H[m] * p.W[m] <= HD_MAXP && p.C[m] % HD_CC == 0, "ssd_heads: maps <= 100 pixels, C % 32 == 0");
+        EDGEDET_REQUIRE(((uintptr_t)p.feat[m] & 15) == 0, "ssd_heads: feature maps 16-byte aligned");
     }
     const int ntiles = (6 * p.cols + HD_NT - 1) / HD_NT;
     hipLaunchKernelGGL(ssd_heads_kernel, dim3((unsigned)(p.nmaps * ntiles), (unsigned)p.B), dim3(256), 0, s, p);
@@ -853,28 +797,7 @@ int ssd_heads_launch(const SsdHeadsParams& p, hipStream_t s) {
     return 0;
 }
 
-// LDS bytes the fused front needs (0 = shape not supported); the plan uses it to decide fusion.
-extern "C" int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin) {
-    if (K == 3 && stride == 1) return (int64_t)MbGeom<3, 1>::lds_bytes(Cin);
-    if (K == 3 && stride == 2) return (int64_t)MbGeom<3, 2>::lds_bytes(Cin);
-    if (K == 5 && stride == 1) return (int64_t)MbGeom<5, 1>::lds_bytes(Cin);
-    if (K == 5 && stride == 2) return (int64_t)MbGeom<5, 2>::lds_bytes(Cin);
-    return 0;
-}
-
 int dwconv_launch(const DwParams& p, hipStream_t s) {
-    if (p.w1) {
-        EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y && p.b1, "mbconv_front: null pointer");
-        EDGEDET_REQUIRE(!p.part, "mbconv_front: no SE squeeze");
-        EDGEDET_REQUIRE(p.C % 8 == 0 && p.Cin % 8 == 0 && p.w1_ld % 4 == 0 && p.w1_ld >= p.Cin,
-                        "mbconv_front: C % 8, Cin % 8 and the weight row stride");
-        EDGEDET_REQUIRE(p.pad == (p.K - 1) / 2, "mbconv_front: 'same' padding only");
-        if (p.K == 3 && p.stride == 1) return mbconv_front_launch<3, 1>(p, s);
-        if (p.K == 3 && p.stride == 2) return mbconv_front_launch<3, 2>(p, s);
-        if (p.K == 5 && p.stride == 1) return mbconv_front_launch<5, 1>(p, s);
-        if (p.K == 5 && p.stride == 2) return mbconv_front_launch<5, 2>(p, s);
-        EDGEDET_REQUIRE(false, "mbconv_front: K in {3, 5}, stride in {1, 2}");
-    }
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
     if (p.part) EDGEDET_REQUIRE(p.parts >= 1 && p.parts <= SE_PARTS, "dwconv: 1..16 SE partial sums");
@@ -1392,32 +1315,6 @@ extern "C" int edgedet_roi_align(const float* feat, int64_t B, int64_t H, int64_
     p.sr = sampling_ratio;
     p.out = out;
     return roi_align_launch(p, (hipStream_t)stream);
-}
-
-extern "C" int edgedet_mbconv_front(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w1,
-                                    int64_t w1_ld, const float* b1, int32_t act1, int64_t C, const float* w,
-                                    const float* bias, int32_t K, int32_t stride, int32_t act, float* y, void* stream) {
-    DwParams p{};
-    p.x = x;
-    p.w1 = w1;
-    p.b1 = b1;
-    p.Cin = (int)Cin;
-    p.w1_ld = (int)w1_ld;
-    p.act1 = act1;
-    p.w = w;
-    p.bias = bias;
-    p.y = y;
-    p.B = (int)B;
-    p.H = (int)H;
-    p.W = (int)W;
-    p.C = (int)C;
-    p.K = K;
-    p.stride = stride;
-    p.pad = (K - 1) / 2;
-    p.act = act;
-    p.Ho = (int)((H + 2 * p.pad - K) / stride + 1);
-    p.Wo = (int)((W + 2 * p.pad - K) / stride + 1);
-    return dwconv_launch(p, (hipStream_t)stream);
 }
 
 extern "C" int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,

@@ -48,7 +48,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_mbconv_front_lds", "edgedet_ssd_stem",
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_ssd_stem",
            "edgedet_mlp_state_size", "edgedet_mlp_fit", "edgedet_mlp_predict",
            "edgedet_model_weights_size", "edgedet_model_pack", "edgedet_model_workspace_size", "edgedet_model_prepare",
            "edgedet_model_prepare_host", "edgedet_model_forward", "edgedet_model_max_detections",
@@ -113,7 +113,6 @@ def lib():
     L.edgedet_conv2d_x3.argtypes = [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
                                     _i32, _vp, _vp, _i32, _vp]
     L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
-    L.edgedet_mbconv_front_lds.argtypes = [_i32, _i32, _i64]
     L.edgedet_mlp_state_size.argtypes = [_i32, _vp]
     L.edgedet_mlp_state_size.restype = ctypes.c_int64
     L.edgedet_mlp_fit.argtypes = [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -146,9 +145,6 @@ def lib():
     L.edgedet_frcnn_workspace_size.restype = _i64
     L.edgedet_frcnn_forward.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.edgedet_ssd_stem.argtypes = [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]
-    L.edgedet_mbconv_front_lds.restype = ctypes.c_int64
-    L.edgedet_mbconv_front.argtypes = [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _i32, _i64, _vp, _vp, _i32, _i32,
-                                       _i32, _vp, _vp]
     L.edgedet_box_correct.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _dbl, _vp, _i64, _vp]
     L.edgedet_orie_ap.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _vp]
     L.edgedet_map_eval.argtypes = [_vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]
@@ -163,7 +159,7 @@ def lib():
     L.edgedet_target.restype = ctypes.c_char_p
     for name in ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
                  "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_dwconv2d", "edgedet_conv2d_ex", "edgedet_split_bf16x3", "edgedet_box_correct", "edgedet_orie_ap",
-           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_mbconv_front", "edgedet_ssd_stem", "edgedet_mlp_fit",
+           "edgedet_map_eval", "edgedet_output_features", "edgedet_conv2d_x3", "edgedet_ssd_stem", "edgedet_mlp_fit",
                  "edgedet_mlp_predict"):
         getattr(L, name).restype = ctypes.c_int
     _LIB = L
@@ -305,22 +301,6 @@ def ssd_stem_nhwc(x4, w0_packed, b0, wd_taps, bd, w1_packed, b1):
     y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, 16), dtype=torch.float32, device=x4.device)
     check(lib().edgedet_ssd_stem(_ptr(x4), B, H, W, _ptr(w0_packed), w0_packed.shape[1], _ptr(b0), _ptr(wd_taps),
                                  _ptr(bd), _ptr(w1_packed), w1_packed.shape[1], _ptr(b1), _ptr(y), stream_handle()))
-    return y
-
-
-def mbconv_front_nhwc(x, w1_packed, b1, act1, w_taps, bias, k, stride, act):
-    """Fused InvertedResidual front: 1x1 expansion (w1_packed [C][ld] from plan.pack_conv_weight,
-    folded BN, act1) then depthwise k x k / stride (w_taps from plan.pack_dw_weight, act), the
-    expanded tensor kept in LDS (csrc/layers.hip mbconv_front_kernel)."""
-    _need_cuda(x, w1_packed, b1, w_taps, bias)
-    B, H, W, Cin = x.shape
-    C, ld = w1_packed.shape
-    pad = (k - 1) // 2
-    Ho = (H + 2 * pad - k) // stride + 1
-    Wo = (W + 2 * pad - k) // stride + 1
-    y = torch.empty((B, Ho, Wo, C), dtype=torch.float32, device=x.device)
-    check(lib().edgedet_mbconv_front(_ptr(x), B, H, W, Cin, _ptr(w1_packed), ld, _ptr(b1), ACT[act1], C, _ptr(w_taps),
-                                     _ptr(bias), k, stride, ACT[act], _ptr(y), stream_handle()))
     return y
 
 

@@ -263,16 +263,6 @@ int edgedet_conv2d_x3(const float* x, uint16_t* x3, int64_t B, int64_t H, int64_
 int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream);
 
 /*
- * Fused MBConv front: y = act(dw_KxK,stride(act1(x . w1^T + b1)) + bias), "same" padding, with the
- * expanded tensor kept on chip.  x NHWC [B,H,W,Cin] (Cin % 8 == 0); w1 [C][w1_ld] (the packed 1x1
- * conv weight, folded BN); b1 [C]; w [K*K][C]; bias [C]; y [B,Ho,Wo,C] (C % 8 == 0).  K in {3, 5},
- * stride in {1, 2}.  Replaces InvertedResidual's expand + depthwise pair (torchvision
- * mobilenetv3.py, reached from torch_models/detect.py:78).
- */
-int edgedet_mbconv_front(const float* x, int64_t B, int64_t H, int64_t W, int64_t Cin, const float* w1,
-                         int64_t w1_ld, const float* b1, int32_t act1, int64_t C, const float* w,
-                         const float* bias, int32_t K, int32_t stride, int32_t act, float* y, void* stream);
-/*
  * SSDLite stem + first block in one pass: y = proj(relu(dw3x3(s))) + b1 + s with
  * s = hardswish(conv3x3_s2(x) + b0) (torchvision mobilenet_v3_large features.0.0 and .0.1, folded BN).
  * x NHWC4 [B,H,W,4] (the preprocessed image); w0 [16][ld0] packed (kh, kw, ci); wd [9][16];
@@ -302,8 +292,6 @@ int edgedet_mlp_fit(const float* x, int64_t N, int64_t D0, const float* y, const
 /* Eval-mode forward of a trained state (running statistics, no dropout): out[r] = net(x[idx[r]]). */
 int edgedet_mlp_predict(const float* x, int64_t D0, const int32_t* idx, int64_t n, int32_t L, const int32_t* dims,
                         const float* state, float* out, void* stream);
-/* LDS bytes edgedet_mbconv_front needs for (K, stride, Cin); 0 if (K, stride) is not supported. */
-int64_t edgedet_mbconv_front_lds(int32_t K, int32_t stride, int64_t Cin);
 /* Depthwise conv2d (+ folded BN + act).  x NHWC [B,H,W,C]; w [KH*KW][C]; bias [C]. */
 int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C, const float* w,
                      const float* bias, int32_t K, int32_t stride, int32_t pad, int32_t act,

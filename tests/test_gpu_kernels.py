@@ -168,35 +168,6 @@ def test_ssd_stem_matches_torch(B, H, W):
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize("B,H,W,Cin,C,k,s,act1,act2", [
-    (2, 160, 160, 16, 64, 3, 2, "RE", "RE"),   # SSDLite block 0.2 (expand 16 -> 64, dw 3x3 s2)
-    (2, 80, 80, 24, 72, 3, 1, "RE", "RE"),     # block 0.3
-    (2, 40, 40, 40, 240, 3, 2, "HS", "HS"),    # block 0.7
-    (2, 20, 20, 80, 200, 3, 1, "HS", "HS"),    # blocks 0.8 (C % 16 == 8: a half channel chunk)
-    (1, 19, 23, 24, 72, 5, 2, "RE", "RE"),     # odd map, 5x5
-    (2, 13, 11, 40, 120, 5, 1, "HS", "R6"),
-    (3, 1, 1, 16, 64, 3, 2, "RE", "HS"),       # 1x1 map: every tap but the centre is padding
-    (1, 9, 9, 112, 16, 3, 1, None, "RE")])
-def test_mbconv_front_matches_torch(B, H, W, Cin, C, k, s, act1, act2):
-    """Fused expand 1x1 + depthwise (csrc/layers.hip mbconv_front_kernel) against torch fp32 of the
-    unfused pair."""
-    from edgeml_amd import ops
-    from edgeml_amd.plan import pack_conv_weight, pack_dw_weight
-    g = torch.Generator().manual_seed(B * H + C)
-    x = torch.randn(B, Cin, H, W, generator=g)
-    w1 = torch.randn(C, Cin, 1, 1, generator=g) / Cin ** 0.5
-    b1 = torch.randn(C, generator=g) * 0.1
-    w2 = torch.randn(C, 1, k, k, generator=g) / k
-    b2 = torch.randn(C, generator=g) * 0.1
-    e = _act(F.conv2d(x, w1, b1), act1)
-    ref = _act(F.conv2d(e, w2, b2, s, (k - 1) // 2, 1, C), act2)
-    w1p = torch.from_numpy(pack_conv_weight(w1.numpy())[0]).to(DEV)
-    got = ops.mbconv_front_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), w1p, b1.to(DEV), act1,
-                                torch.from_numpy(pack_dw_weight(w2.numpy())).to(DEV), b2.to(DEV), k, s, act2)
-    err = (got.permute(0, 3, 1, 2).cpu() - ref).abs().max().item()
-    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
-
-
 @pytest.mark.parametrize("B,C,S,parts", [(1, 72, 24, 16), (32, 960, 240, 1), (7, 120, 32, 5), (64, 672, 168, 2),
                                           (33, 480, 120, 16)])
 def test_se_excitation_matches_torch(B, C, S, parts):

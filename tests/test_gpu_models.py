@@ -116,7 +116,8 @@ def test_ssd_grouped_small_heads_match_separate_ops(ssd, monkeypatch, B):
         native.release("ssd", B, 480, 640)
         model.plans.clear()
         plan = _run(model, imgs)
-        assert sum(op.kind == 24 for op in plan.ops) == (2 if v == "1" else 0)
+        n_heads = sum(op.kind == 24 for op in plan.ops)  # two per chain (one per branch)
+        assert (n_heads > 0 and n_heads % 2 == 0) if v == "1" else n_heads == 0
         outs[v] = (plan.cls_logits.tensor().cpu(), plan.bbox_regression.tensor().cpu())
     native.release("ssd", B, 480, 640)
     model.plans.clear()

@@ -264,17 +264,6 @@ def test_retina_anchors_match_oracle(hp, wp):
         np.testing.assert_array_equal(a, b.numpy())
 
 
-def test_mbconv_front_lds_formula_matches_library():
-    """models.py decides MBConv fusion with a restatement of the kernel's LDS size (csrc/layers.hip
-    MbGeom); both must agree on every shape SSDLite lowers."""
-    from edgeml_amd import ops
-    L = ops.lib()
-    for k, s, cin in [(3, 2, 16), (3, 1, 24), (3, 2, 40), (3, 1, 80), (5, 2, 24), (5, 1, 40), (3, 1, 112)]:
-        ipp = ((7 * s + k) ** 2 + 31) // 32 * 32
-        assert L.edgedet_mbconv_front_lds(k, s, cin) == 4 * (ipp * (cin + 4) + 32 * (cin + 4) + ipp * 36)
-    assert L.edgedet_mbconv_front_lds(7, 1, 16) == 0
-
-
 def test_estimator_state_layout_matches_library():
     """edgeml_amd.estimator.MlpSpec and csrc/estimator.hip mlp_layout agree on the state size."""
     import ctypes

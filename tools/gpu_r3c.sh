@@ -12,4 +12,6 @@ for cfg in "0 0" "0 1" "1 1" "1 0"; do
       --dump-ops gpurun_out/ops_mb$1_h$2.json > gpurun_out/bench_mb$1_h$2.log 2>&1 || { echo "bench $cfg failed" >> gpurun_out/r3c.txt; exit 1; }
   echo "mb=$1 heads=$2 $(tail -1 gpurun_out/bench_mb$1_h$2.log | cut -c1-200)" >> gpurun_out/r3c.txt
 done
+timeout -k 10 300 python -u bench.py --model frcnn --no-cpu --no-e2e --dump-ops gpurun_out/ops_frcnn.json > gpurun_out/bench_frcnn.log 2>&1 || { echo "frcnn bench failed" >> gpurun_out/r3c.txt; exit 1; }
+echo "frcnn $(tail -1 gpurun_out/bench_frcnn.log | cut -c1-300)" >> gpurun_out/r3c.txt
 timeout -k 10 600 python -u tools/ingest_bench.py --n 2000 > gpurun_out/ingest.log 2>&1; echo "ingest rc=$?" >> gpurun_out/r3c.txt
