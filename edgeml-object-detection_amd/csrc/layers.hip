@@ -424,13 +424,13 @@ extern "C" int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W,
 // 0.2 / 0.3 at 160^2 / 80^2): expand 1x1 (+ folded BN, act), depthwise KxK stride S (+ folded BN, act),
 // project 1x1 (+ folded BN), + the block input when S == 1 and Cin == Cout.  Neither the 3-4x-wide
 // expanded tensor nor the depthwise output reaches HBM.  Block = one image, an 8 x 8 output tile,
-// 4 waves; the expanded channels are processed in chunks of 32 through LDS:
+// 8 waves; the expanded channels are processed in chunks of 32 through LDS:
 //   expand   v_mfma_f32_32x32x2_f32 (exact fp32 products): [halo pixels, 32-row tiles over the waves]
 //            x [Cin] x [32 channels]; + bias, act; halo pixels outside the image are zero (the
 //            depthwise conv pads the expanded tensor with zeros);
 //   depthwise VALU from LDS, taps in (kh, kw) order, + bias, act;
 //   project  v_mfma_f32_32x32x2_f32: [64 output pixels] x [32 chunk channels] x [Cout], accumulated in
-//            registers over the chunks (waves own (pixel tile, Cout tile) pairs).
+//            registers over the chunks (waves own (pixel tile, K quarter) pairs).
 // The round-2 form (expansion and projection on the VALU, one pixel x channel per thread) measured
 // 3.5-4.5x slower than the three separate ops; the matrix-core form keeps each phase to a few MFMAs
 // per wave.
@@ -444,24 +444,26 @@ struct MbfGeom {
     static constexpr int ES = MBF_CC + 1;  // expanded chunk row pitch
 };
 
-// NCO: 32-wide Cout tiles (Cout <= 32 * NCO; the launcher instantiates NCO = 1).  A chunk's weights
-// (expand rows, project columns, depthwise taps, biases) are loaded into registers one chunk ahead, all
-// loads of a thread issued together, and stored to LDS at the chunk boundary; the projection's two
-// 32-pixel tiles are split over the four waves by K half (waves 2, 3 take channels 16..31 of each
-// chunk), and the two halves are added once at the end (fixed order).
+// NCO: 32-wide Cout tiles (Cout <= 32 * NCO; the launcher instantiates NCO = 1).  8 waves (16 per CU
+// at two workgroups, to cover the halo and weight loads).  A chunk's weights (expand rows, project
+// columns, depthwise taps, biases) are loaded into registers one chunk ahead, all loads of a thread
+// issued together, and stored to LDS at the chunk boundary; the projection's two 32-pixel tiles are
+// split over the eight waves by K quarter (wave w: tile w & 1, channels 8 (w >> 1) .. + 7 of each
+// chunk), and the quarters are added once at the end in a fixed order ((q0 + q2) + (q1 + q3)).
 template <int K, int S, int ACT, int CINP, int NCO>
-__global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
+__global__ void __launch_bounds__(512) mbconv_kernel(MbParams p, int tiles_w) {
     static_assert(NCO == 1, "mbconv: the K-split projection is laid out for one Cout tile");
     using G = MbfGeom<K, S, CINP>;
     constexpr int IH = G::IH, NPX = G::NPX, NPXP = G::NPXP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
     __shared__ float xs[NPXP * XS];        // input halo [pixel][Cin] (rows past NPX zero)
-    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]; at the end the K-half partials
+    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]; at the end the K-quarter partials
     __shared__ float ds[TT * ES];          // depthwise chunk [output pixel][32]
     __shared__ float w1s[MBF_CC * XS];     // expand weights of the chunk [32][Cin]
     __shared__ float w2s[32 * NCO * ES];   // project weights of the chunk [Cout pad][32]
     __shared__ float wds[K * K * MBF_CC];  // depthwise taps of the chunk [tap][32]
     __shared__ float b1s[MBF_CC], bds[MBF_CC];
-    static_assert(2 * 64 * 16 <= NPXP * ES, "K-half partials fit the expanded-chunk buffer");
+    static_assert(4 * 64 * 16 <= NPXP * ES, "two K-quarter partial pairs fit the expanded-chunk buffer");
+    constexpr int NT = 512, NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, h = lane >> 5;
     const int b = blockIdx.y;
     const int oh0 = (blockIdx.x / tiles_w) * MBF_T, ow0 = (blockIdx.x % tiles_w) * MBF_T;
@@ -470,22 +472,22 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
     const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
     // chunk operands in registers (zero past Cexp / Cin / Cout)
     constexpr int N1 = MBF_CC * CINP, N2 = 32 * NCO * MBF_CC, ND = K * K * MBF_CC + 2 * MBF_CC;
-    constexpr int U1 = (N1 + 255) / 256, U2 = (N2 + 255) / 256, UD = (ND + 255) / 256;
+    constexpr int U1 = (N1 + NT - 1) / NT, U2 = (N2 + NT - 1) / NT, UD = (ND + NT - 1) / NT;
     float r1[U1], r2[U2], rd[UD];
     auto load_chunk = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < U1; ++u) {
-            const int t = tid + 256 * u, n = t / CINP, c = t - n * CINP;
+            const int t = tid + NT * u, n = t / CINP, c = t - n * CINP;
             r1[u] = (t < N1 && c0 + n < Cexp && c < Cin) ? p.w1[(int64_t)(c0 + n) * p.ld1 + c] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
-            const int t = tid + 256 * u, co = t / MBF_CC, j = t - co * MBF_CC;
+            const int t = tid + NT * u, co = t / MBF_CC, j = t - co * MBF_CC;
             r2[u] = (t < N2 && co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
-            const int t = tid + 256 * u;
+            const int t = tid + NT * u;
             float v = 0.f;
             if (t < K * K * MBF_CC) {
                 const int tap = t / MBF_CC, j = t - tap * MBF_CC;
@@ -503,17 +505,17 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
     auto store_chunk = [&]() {
 #pragma unroll
         for (int u = 0; u < U1; ++u) {
-            const int t = tid + 256 * u, n = t / CINP, c = t - n * CINP;
+            const int t = tid + NT * u, n = t / CINP, c = t - n * CINP;
             if (t < N1) w1s[n * XS + c] = r1[u];
         }
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
-            const int t = tid + 256 * u, co = t / MBF_CC, j = t - co * MBF_CC;
+            const int t = tid + NT * u, co = t / MBF_CC, j = t - co * MBF_CC;
             if (t < N2) w2s[co * ES + j] = r2[u];
         }
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
-            const int t = tid + 256 * u;
+            const int t = tid + NT * u;
             if (t < K * K * MBF_CC) wds[t] = rd[u];
             else if (t < K * K * MBF_CC + MBF_CC) b1s[t - K * K * MBF_CC] = rd[u];
             else if (t < ND) bds[t - K * K * MBF_CC - MBF_CC] = rd[u];
@@ -522,11 +524,11 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
     load_chunk(0);
     // 1. input halo (zero outside the image and past Cin), all loads of a thread in flight together
     {
-        constexpr int N = NPXP * CINP, U = (N + 255) / 256;
+        constexpr int N = NPXP * CINP, U = (N + NT - 1) / NT;
         float v[U];
 #pragma unroll
         for (int r = 0; r < U; ++r) {
-            const int t = tid + 256 * r;
+            const int t = tid + NT * r;
             const int px = t / CINP, c = t - px * CINP;
             const int ih = ih0 + px / IH, iw = iw0 + px % IH;
             const bool in = t < N && px < NPX && c < Cin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
@@ -534,21 +536,21 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
         }
 #pragma unroll
         for (int r = 0; r < U; ++r) {
-            const int t = tid + 256 * r;
+            const int t = tid + NT * r;
             if (t < N) xs[(t / CINP) * XS + t % CINP] = v[r];
         }
     }
     mbf_floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int pt = wid & 1, kh0 = 16 * (wid >> 1);  // projection: pixel tile, K half of the chunk
+    const int pt = wid & 1, kq = wid >> 1, kh0 = 8 * kq;  // projection: pixel tile, K quarter of the chunk
     for (int c0 = 0; c0 < Cexp; c0 += MBF_CC) {
         __syncthreads();  // xs written; the previous chunk's es / ds / weights consumed
         store_chunk();
         if (c0 + MBF_CC < Cexp) load_chunk(c0 + MBF_CC);  // in flight under this chunk's three phases
         __syncthreads();
-        // 2. expand: wave w takes 32-pixel row tiles w, w + 4, ...
-        for (int t = wid; t < NPXP / 32; t += 4) {
+        // 2. expand: wave w takes 32-pixel row tiles w, w + 8, ...
+        for (int t = wid; t < NPXP / 32; t += NW) {
             mbf_floatx16 e;
 #pragma unroll
             for (int r = 0; r < 16; ++r) e[r] = 0.f;
@@ -566,7 +568,7 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
             }
         }
         __syncthreads();
-        // 3. depthwise: thread = (channel tid & 31, output pixels (tid >> 5) + 8 j)
+        // 3. depthwise: thread = (channel tid & 31, output pixels (tid >> 5) + 16 j)
         {
             const int ch = tid & 31;
             float wt[K * K];
@@ -574,8 +576,8 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
             for (int q = 0; q < K * K; ++q) wt[q] = wds[q * MBF_CC + ch];
             const float bd = bds[ch];
 #pragma unroll
-            for (int j = 0; j < TT / 8; ++j) {
-                const int op = (tid >> 5) + 8 * j;
+            for (int j = 0; j < TT / 16; ++j) {
+                const int op = (tid >> 5) + 16 * j;
                 const int ly = op / MBF_T, lx = op % MBF_T;
                 float a = 0.f;
 #pragma unroll
@@ -586,21 +588,32 @@ __global__ void __launch_bounds__(256) mbconv_kernel(MbParams p, int tiles_w) {
             }
         }
         __syncthreads();
-        // 4. project: wave w = (pixel tile w & 1, K half w >> 1) over the Cout tile
+        // 4. project: wave w = (pixel tile w & 1, K quarter w >> 1) over the Cout tile
         {
             const float* ar = ds + (32 * pt + l32) * ES + kh0 + h;
             const float* br = w2s + l32 * ES + kh0 + h;
 #pragma unroll
-            for (int k = 0; k < MBF_CC / 2; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc, 0, 0, 0);
+            for (int k = 0; k < MBF_CC / 4; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc, 0, 0, 0);
         }
     }
-    // 5. the upper K half's partials through LDS (es is free: every wave is past the last depthwise)
-    if (wid >= 2) {
+    // 5. the K quarters through LDS (es is free: every wave is past the last depthwise): quarters 2, 3
+    //    into 0, 1, then 1 into 0
+    if (kq >= 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) es[((wid - 4) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (kq < 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += es[(wid * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+    if (kq == 1) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) es[((wid - 2) * 16 + r) * 64 + lane] = acc[r];
     }
     __syncthreads();
-    if (wid >= 2) return;
+    if (kq != 0) return;
     // 6. bias, residual, store (lane = output channel, registers = output pixels)
     const int co = l32;
     if (co >= Cout) return;
@@ -621,9 +634,9 @@ static int mbconv_launch_kc(const MbParams& p, hipStream_t s) {
     const int tiles_w = cdiv(p.Wo, MBF_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, MBF_T) * tiles_w), (unsigned)p.B);
     switch (p.act) {
-        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
-        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
-        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINP, NCO>), grid, dim3(256), 0, s, p, tiles_w); break;
+        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
+        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
+        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
         default: EDGEDET_REQUIRE(false, "mbconv: activation RE / R6 / HS");
     }
     EDGEDET_LAUNCH_CHECK();
@@ -855,57 +868,59 @@ int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStr
 constexpr int SE1_BB = 8, SE1_SB = 8, SE2_BB = 8, SE2_SCH = 128;
 constexpr int SE_CMAX = 1024, SE_SMAX = 512;
 
-// LDS staging with SE_U independent loads in flight per thread (a plain strided loop waits for
+// LDS staging with SE_U independent 16-byte loads in flight per thread (a plain strided loop waits for
 // every load before issuing the next: one memory round trip per element, which dominated these
-// latency-bound kernels).  dst[t] = src(t) for t < n; with ACC, dst[t] += src(t).
+// latency-bound kernels).  dst (16-byte aligned) as f32x4 [t] = src4(t) for t < n4.
 constexpr int SE_U = 8;
-template <bool ACC, typename F>
-__device__ __forceinline__ void se_stage(float* dst, int n, F src) {
-    for (int base = threadIdx.x; base < n; base += 256 * SE_U) {
-        float v[SE_U];
+template <typename F>
+__device__ __forceinline__ void se_stage4(float* dst, int n4, F src4) {
+    for (int base = threadIdx.x; base < n4; base += 256 * SE_U) {
+        f32x4 v[SE_U];
 #pragma unroll
         for (int u = 0; u < SE_U; ++u) {
             const int t = base + 256 * u;
-            v[u] = t < n ? src(t) : 0.f;
+            v[u] = t < n4 ? src4(t) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < SE_U; ++u) {
             const int t = base + 256 * u;
-            if (t < n) dst[t] = ACC ? dst[t] + v[u] : v[u];
+            if (t < n4) reinterpret_cast<f32x4*>(dst)[t] = v[u];
         }
     }
 }
 
-// ms[bl * C + c] = mean over the squeeze partial sums of image b0 + bl, summed in part order; the
-// loads of SE_U elements x 4 parts are issued together.
+// ms[bl * C + c] = mean over the squeeze partial sums of image b0 + bl, summed in part order; each
+// thread takes four channels (C % 4 == 0), and the loads of SE_U quads x 4 parts are issued together.
 __device__ __forceinline__ void se_stage_means(float* ms, const float* __restrict__ part, int b0, int nb, int C,
                                                int parts, float inv) {
-    const int n = nb * C;
-    for (int base = threadIdx.x; base < n; base += 256 * SE_U) {
+    const int C4 = C >> 2, n4 = nb * C4;
+    for (int base = threadIdx.x; base < n4; base += 256 * SE_U) {
         const float* src[SE_U];
-        float acc[SE_U];
+        f32x4 acc[SE_U];
 #pragma unroll
         for (int u = 0; u < SE_U; ++u) {
-            const int t = min(base + 256 * u, n - 1);
-            const int bl = t / C, c = t - bl * C;
-            src[u] = part + (int64_t)(b0 + bl) * parts * C + c;
-            acc[u] = 0.f;
+            const int t = min(base + 256 * u, n4 - 1);
+            const int bl = t / C4, c4 = t - bl * C4;
+            src[u] = part + (int64_t)(b0 + bl) * parts * C + 4 * c4;
+            acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         for (int k0 = 0; k0 < parts; k0 += 4) {
-            float v[SE_U][4];
+            f32x4 v[SE_U][4];
 #pragma unroll
             for (int u = 0; u < SE_U; ++u)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[u][q] = src[u][(int64_t)min(k0 + q, parts - 1) * C];
+                for (int q = 0; q < 4; ++q)
+                    v[u][q] = *reinterpret_cast<const f32x4*>(src[u] + (int64_t)min(k0 + q, parts - 1) * C);
 #pragma unroll
             for (int u = 0; u < SE_U; ++u)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc[u] += k0 + q < parts ? v[u][q] : 0.f;
+                for (int q = 0; q < 4; ++q)
+                    if (k0 + q < parts) acc[u] += v[u][q];
         }
 #pragma unroll
         for (int u = 0; u < SE_U; ++u) {
             const int t = base + 256 * u;
-            if (t < n) ms[t] = acc[u] * inv;
+            if (t < n4) reinterpret_cast<f32x4*>(ms)[t] = acc[u] * inv;
         }
     }
 }
@@ -913,13 +928,13 @@ __device__ __forceinline__ void se_stage_means(float* ms, const float* __restric
 __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ part, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, float* __restrict__ hidden, int B,
                                                      int C, int S, int HW, int parts) {
-    __shared__ float ms[SE1_BB * SE_CMAX];
-    __shared__ float ws[SE1_SB * SE_CMAX];
+    __shared__ __attribute__((aligned(16))) float ms[SE1_BB * SE_CMAX];
+    __shared__ __attribute__((aligned(16))) float ws[SE1_SB * SE_CMAX];
     const int s0 = blockIdx.x * SE1_SB, b0 = blockIdx.y * SE1_BB;
     const int nb = min(SE1_BB, B - b0), ns = min(SE1_SB, S - s0);
     const float inv = 1.f / (float)HW;
     se_stage_means(ms, part, b0, nb, C, parts, inv);  // each thread rewrites only its own elements
-    se_stage<false>(ws, ns * C, [&](int t) { return w1[(int64_t)s0 * C + t]; });
+    se_stage4(ws, ns * C / 4, [&](int t) { return *reinterpret_cast<const f32x4*>(w1 + (int64_t)s0 * C + 4 * t); });
     __syncthreads();
     // 64 outputs (bl = o & 7, sl = o >> 3), 4 threads each over C quarters
     const int o = threadIdx.x >> 2, h = threadIdx.x & 3;
@@ -944,20 +959,21 @@ __global__ void __launch_bounds__(256) se_fc1_kernel(const float* __restrict__ p
 __global__ void __launch_bounds__(256) se_fc2_kernel(const float* __restrict__ hidden, const float* __restrict__ w2t,
                                                      const float* __restrict__ b2, float* __restrict__ scale, int B,
                                                      int C, int S) {
-    __shared__ float hs[SE2_BB * SE_SMAX];
-    __shared__ float ws[SE2_SCH * 64];
+    __shared__ __attribute__((aligned(16))) float hs[SE2_BB * SE_SMAX];
+    __shared__ __attribute__((aligned(16))) float ws[SE2_SCH * 64];
     const int c0 = blockIdx.x * 64, b0 = blockIdx.y * SE2_BB;
     const int nb = min(SE2_BB, B - b0), nc = min(64, C - c0);
-    se_stage<false>(hs, nb * S, [&](int t) { return hidden[(int64_t)b0 * S + t]; });
+    se_stage4(hs, nb * S / 4, [&](int t) { return *reinterpret_cast<const f32x4*>(hidden + (int64_t)b0 * S + 4 * t); });
     const int cl = threadIdx.x & 63, bp = threadIdx.x >> 6;  // images bp and bp + 4
     float a0 = 0.f, a1 = 0.f;
     const float* h0 = hs + bp * S;
     const float* h1 = hs + (bp + 4) * S;
     for (int j0 = 0; j0 < S; j0 += SE2_SCH) {
         const int nj = min(SE2_SCH, S - j0);
-        se_stage<false>(ws, nj * 64, [&](int t) {
-            const int j = t >> 6, c = t & 63;
-            return c < nc ? w2t[(int64_t)(j0 + j) * C + c0 + c] : 0.f;
+        se_stage4(ws, nj * 16, [&](int t) {  // 16 quads per 64-channel row; quads past C read as zero
+            const int j = t >> 4, c = 4 * (t & 15);
+            return c < nc ? *reinterpret_cast<const f32x4*>(w2t + (int64_t)(j0 + j) * C + c0 + c)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
         });
         __syncthreads();
 #pragma unroll 8
@@ -1048,6 +1064,9 @@ int se_fc_launch(const float* part, const float* w1, const float* b1, const floa
     EDGEDET_REQUIRE(parts >= 1 && parts <= SE_PARTS, "se_fc: 1..16 squeeze partial sums");
     EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
     EDGEDET_REQUIRE(S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX && HW >= 1, "se_fc: C <= 1024, S <= 512");
+    EDGEDET_REQUIRE(C % 4 == 0 && S % 4 == 0 && ((uintptr_t)part & 15) == 0 && ((uintptr_t)w1 & 15) == 0 &&
+                        ((uintptr_t)w2t & 15) == 0 && ((uintptr_t)hidden & 15) == 0,
+                    "se_fc: C % 4, S % 4 and 16-byte aligned partial sums / weights / hidden (16-byte staging)");
     hipLaunchKernelGGL(se_fc1_kernel, dim3((unsigned)cdiv(S, SE1_SB), (unsigned)cdiv(B, SE1_BB)), dim3(256), 0, s,
                        part, w1, b1, hidden, B, C, S, HW, parts);
     EDGEDET_LAUNCH_CHECK();

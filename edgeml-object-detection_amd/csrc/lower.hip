@@ -820,9 +820,11 @@ class SSDLite {
         int64_t off = 0;
         if (nch == 1) P.fork(3);
         int br = 0;
-        // maps 1..5 (10x10 and below) as one SSD_HEADS launch per branch (EDGEDET_SSD_HEADS=0: the
-        // separate depthwise + 1x1 pair per map and branch)
-        const bool group = !pack_only && env_int("EDGEDET_SSD_HEADS", 1) == 1;
+        // EDGEDET_SSD_HEADS=1: maps 1..5 (10x10 and below) as one SSD_HEADS launch per branch.  Off by
+        // default: measured 23.7k against 27.3k img/s (r3e) — one workgroup walks its map's channels
+        // in 15 dependent chunks, so under the other chains' HBM traffic the launch takes ~250 us, where
+        // the ten separate depthwise + 1x1 launches each take one memory round trip.
+        const bool group = !pack_only && env_int("EDGEDET_SSD_HEADS", 0) == 1;
         OpRec grp[2];
         for (int h = 0; h < 2; ++h) {
             grp[h].kind = EDGEDET_OP_SSD_HEADS;

@@ -161,7 +161,7 @@ def test_ssd_plan_lowering():
     mb = kinds.count(ops.MBCONV)
     assert mb == (2 if os.environ.get("EDGEDET_MB_BLOCK") == "1" else 0)
     # the head branches of maps 1..5 as one SSD_HEADS op per branch (10 depthwise + 10 convs fewer)
-    grouped = os.environ.get("EDGEDET_SSD_HEADS") != "0"
+    grouped = os.environ.get("EDGEDET_SSD_HEADS") == "1"
     assert kinds.count(ops.SSD_HEADS) == (2 if grouped else 0)
     heads = 2 if grouped else 12
     assert n_dw == 15 + 4 + heads - stem - mb
