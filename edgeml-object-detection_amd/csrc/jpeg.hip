@@ -17,8 +17,11 @@
 // (progressive, arithmetic coding, 12-bit, CMYK / RGB JPEGs, other samplings) reports "unsupported" and
 // the caller decodes that image on the host.
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.hpp"
@@ -104,6 +107,20 @@ struct BitReader {
     int bits = 0;
     bool marker = false;  // hit a marker: feed zeros (libjpeg's behaviour at a premature marker)
     void fill() {
+        // fast path: the next 8 bytes hold no 0xFF (no stuffing, no marker): take the whole bytes that fit
+        if (!marker && pos + 8 <= n) {
+            uint64_t x;
+            std::memcpy(&x, d + pos, 8);
+            x = __builtin_bswap64(x);
+            const uint64_t nx = ~x;
+            if (((nx - 0x0101010101010101ull) & ~nx & 0x8080808080808080ull) == 0) {
+                const int nb = (64 - bits) >> 3;  // >= 1 (bits <= 56 here)
+                acc |= (x >> (64 - 8 * nb)) << (64 - bits - 8 * nb);
+                bits += 8 * nb;
+                pos += (size_t)nb;
+                return;
+            }
+        }
         while (bits <= 56) {
             uint32_t byte = 0;
             if (!marker && pos < n) {
@@ -185,13 +202,14 @@ struct Decoder {
     int adobe_transform = -1;
     bool jfif = false;
 
-    int64_t run(const uint8_t* d, size_t n, std::vector<uint8_t>& out) {
+    // Parses and entropy-decodes into hd / binfo (per block: start, count) / coef (the caller's
+    // scratch, reused across calls); returns the packet's byte size (write() lays it out).
+    Header hd{};
+    int64_t run(const uint8_t* d, size_t n, std::vector<uint32_t>& binfo, std::vector<uint32_t>& coef) {
         if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return fail("not a JPEG (no SOI)");
         size_t pos = 2;
         bool have_frame = false;
-        std::vector<uint32_t> binfo;  // per block: start, count
-        std::vector<uint32_t> coef;
-        Header hd{};
+        hd = Header{};
         while (pos + 4 <= n) {
             if (d[pos] != 0xFF) {
                 ++pos;
@@ -268,7 +286,7 @@ struct Decoder {
                 hd.nblocks = nb;
                 binfo.assign((size_t)2 * nb, 0u);
                 coef.clear();
-                coef.reserve((size_t)nb * 12);
+                coef.reserve((size_t)nb * 24);
                 have_frame = true;
             } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
                 return unsupported("progressive / lossless / arithmetic-coded JPEG");
@@ -348,12 +366,14 @@ struct Decoder {
         const int64_t bytes = (int64_t)hd.off_coef + 4 * (int64_t)coef.size();
         if (bytes > 0x7fffffff) return fail("packet too large");
         hd.bytes = (int32_t)bytes;
-        out.resize((size_t)bytes);
-        std::memset(out.data(), 0, (size_t)hd.off_blocks);
-        std::memcpy(out.data(), &hd, sizeof(Header));
-        std::memcpy(out.data() + hd.off_blocks, binfo.data(), 4 * binfo.size());
-        if (!coef.empty()) std::memcpy(out.data() + hd.off_coef, coef.data(), 4 * coef.size());
         return bytes;
+    }
+
+    void write(uint8_t* out, const std::vector<uint32_t>& binfo, const std::vector<uint32_t>& coef) const {
+        std::memset(out, 0, (size_t)hd.off_blocks);
+        std::memcpy(out, &hd, sizeof(Header));
+        std::memcpy(out + hd.off_blocks, binfo.data(), 4 * (size_t)2 * hd.nblocks);
+        if (!coef.empty()) std::memcpy(out + hd.off_coef, coef.data(), 4 * coef.size());
     }
 
     // one scan; returns bytes consumed (up to the next marker that is not RST)
@@ -620,9 +640,10 @@ using namespace edgedet::jpeg;
 // host; edgedet_last_error says why), < 0 = malformed data.  Thread-safe; host only.
 extern "C" int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* out, int64_t cap, int32_t* hw) {
     EDGEDET_REQUIRE(data && size > 0, "jpeg_packet: empty input");
+    // per-thread scratch, kept across calls (a host thread decodes file after file)
+    static thread_local std::vector<uint32_t> binfo, coef;
     Decoder dec;
-    std::vector<uint8_t> pkt;
-    const int64_t n = dec.run(data, (size_t)size, pkt);
+    const int64_t n = dec.run(data, (size_t)size, binfo, coef);
     if (n <= 0) {
         set_error("edgedet: jpeg: " + dec.err);
         return n;
@@ -631,8 +652,84 @@ extern "C" int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* 
         hw[0] = dec.H;
         hw[1] = dec.W;
     }
-    if (out && cap >= n) std::memcpy(out, pkt.data(), (size_t)n);
+    if (out && cap >= n) dec.write(static_cast<uint8_t*>(out), binfo, coef);
     return n;
+}
+
+// (H, W) of an image file from its header, as PIL's Image.open(path).size reports it (detect.py's
+// read_image shapes; EXIF orientation is not applied by either): JPEG from the first SOFn segment, PNG
+// from IHDR.  1 = found, 0 = another format or no SOF in the first 1 MiB (the caller asks PIL).
+static int image_dims(const char* path, int32_t* hw) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return 0;
+    uint8_t buf[65536];
+    size_t want = 4096;  // the frame header is usually in the first few hundred bytes
+    size_t n = std::fread(buf, 1, want, f);
+    bool eof = n < want;
+    int found = 0;
+    if (n >= 24 && std::memcmp(buf, "\x89PNG\r\n\x1a\n", 8) == 0 && std::memcmp(buf + 12, "IHDR", 4) == 0) {
+        hw[1] = (int32_t)(((uint32_t)buf[16] << 24) | ((uint32_t)buf[17] << 16) | ((uint32_t)buf[18] << 8) | buf[19]);
+        hw[0] = (int32_t)(((uint32_t)buf[20] << 24) | ((uint32_t)buf[21] << 16) | ((uint32_t)buf[22] << 8) | buf[23]);
+        found = 1;
+    } else if (n >= 4 && buf[0] == 0xFF && buf[1] == 0xD8) {
+        // walk the marker segments; a segment may straddle the buffer end: refill from its start
+        size_t base = 0, pos = 2;  // file offset of buf[0]; position in buf
+        for (int guard = 0; guard < 4096 && !found; ++guard) {
+            if (pos + 9 > n) {
+                if (eof || base + pos > (1u << 20)) break;
+                base += pos;
+                if (std::fseek(f, (long)base, SEEK_SET) != 0) break;
+                want = sizeof(buf);
+                n = std::fread(buf, 1, want, f);
+                eof = n < want;
+                pos = 0;
+                if (n < 9) break;
+            }
+            if (buf[pos] != 0xFF) break;
+            const int m = buf[pos + 1];
+            if (m == 0xFF) {  // fill byte
+                ++pos;
+                continue;
+            }
+            if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) {  // no length
+                pos += 2;
+                continue;
+            }
+            const size_t len = ((size_t)buf[pos + 2] << 8) | buf[pos + 3];
+            if (m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+                hw[0] = (int32_t)(((uint32_t)buf[pos + 5] << 8) | buf[pos + 6]);
+                hw[1] = (int32_t)(((uint32_t)buf[pos + 7] << 8) | buf[pos + 8]);
+                found = hw[0] > 0 && hw[1] > 0;
+                break;
+            }
+            if (m == 0xD9 || m == 0xDA || len < 2) break;  // EOI / scan before any frame header
+            pos += 2 + len;
+        }
+    }
+    std::fclose(f);
+    return found;
+}
+
+// Header dims of n files on `threads` host threads (0 = hardware concurrency): hw[2i..2i+1] = (H, W),
+// or (0, 0) where the header was not understood.  Returns how many were found.
+extern "C" int64_t edgedet_image_dims(const char* const* paths, int64_t n, int32_t* hw, int32_t threads) {
+    EDGEDET_REQUIRE(n >= 0 && (n == 0 || (paths && hw)), "image_dims: null arguments");
+    int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nt = (int)std::min<int64_t>(nt, std::max<int64_t>(1, n / 16));
+    std::atomic<int64_t> next{0}, found{0};
+    auto work = [&] {
+        int64_t k;
+        while ((k = next.fetch_add(64)) < n)
+            for (int64_t i = k; i < std::min<int64_t>(n, k + 64); ++i) {
+                hw[2 * i] = hw[2 * i + 1] = 0;
+                if (paths[i] && image_dims(paths[i], hw + 2 * i)) found.fetch_add(1);
+            }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return found.load();
 }
 
 // Plane scratch bytes one image of the batch needs: the largest nblocks * 64 over the packets is what

@@ -90,12 +90,25 @@ def _image_size(path):
 
 
 def image_sizes(dataset, workers=None):
-    """(H, W) of every image of the dataset, from the file headers (no decode), on a thread pool."""
+    """(H, W) of every image of the dataset, from the file headers (no decode): JPEG / PNG headers parsed
+    natively on host threads (edgedet_image_dims), any other file through PIL's header reader."""
+    import ctypes
     import concurrent.futures as cf
+    from . import ops
     from .distributed import usable_cpus
     paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
-    with cf.ThreadPoolExecutor(workers or usable_cpus()) as ex:
-        return list(ex.map(_image_size, paths))
+    n = len(paths)
+    hw = np.zeros((n, 2), np.int32)
+    if n:
+        arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+        ops.lib().edgedet_image_dims(ctypes.cast(arr, ctypes.c_void_p), n, hw.ctypes.data, workers or usable_cpus())
+    sizes = [(int(h), int(w)) for h, w in hw]
+    rest = [i for i, (h, w) in enumerate(sizes) if h <= 0 or w <= 0]
+    if rest:
+        with cf.ThreadPoolExecutor(workers or usable_cpus()) as ex:
+            for i, s in zip(rest, ex.map(_image_size, [paths[i] for i in rest])):
+                sizes[i] = s
+    return sizes
 
 
 def _packet_or_none(path):
@@ -106,7 +119,7 @@ def _packet_or_none(path):
         data = f.read()
     if data[:2] != b"\xff\xd8":
         return None
-    pk, _ = jpeg.packet(data)
+    pk, _ = jpeg.packet(data, pinned=torch.cuda.is_available())
     return pk
 
 
@@ -163,6 +176,8 @@ def detect_rows(model, images, dataset="coco"):
 
 def main(opts):
     from . import distributed as dist_mod
+    import time
+    clock = [("start", time.perf_counter())]  # EDGEDET_DETECT_TIMING=1: phase times to stderr
     img_names = sorted(os.listdir(opts.img_dir))
     if not torch.cuda.is_available():
         raise RuntimeError("edgeml_amd.detect needs an MI355X (HIP) device; there is no CPU path")
@@ -175,6 +190,7 @@ def main(opts):
         print(f"Using {device} device (world {world})")
     model = load_weak_models(opts.model, opts.model_path, num_class).to(device)
     model.eval()
+    clock.append(("model", time.perf_counter()))
     Path(opts.save_dir).mkdir(parents=True, exist_ok=True)
     batch = min(getattr(opts, "batch", None) or model.max_batch, model.max_batch)
     results = {}
@@ -185,20 +201,34 @@ def main(opts):
     # batches on the device at once (run_batches), so one batch's NMS tail overlaps the next
     # batch's backbone.
     sizes = image_sizes(dataset)
+    clock.append(("sizes", time.perf_counter()))
     chunks = dist_mod.size_batches(sizes, batch)
     shards = [dist_mod.batch_shard(chunks, r, world) for r in range(world)]
     shard_names = [[img_names[i] for c in sh for i in c] for sh in shards]
     my_names = shard_names[rank]
     tagged = (((names, hw), buf) for names, hw, buf in
               _decoded_batches(dataset, shards[rank], sizes, device_decode=getattr(opts, "decode", "gpu") == "gpu"))
-    for (names, (h, w)), counts, boxes, scores, labels in model.run_batches(tagged, raw=True):
-        for name, rows in zip(names, fmt.format_batch(boxes, scores, labels, counts, h, w, opts.dataset)):
-            results[name] = rows
-    if world > 1:
-        results = dist_mod.gather_rows(results, my_names, img_names, rank, world, shards=shard_names)
-    if rank == 0:
-        for name in img_names:
-            fmt.save_npy(opts.save_dir, name, results[name])
+    # the .npy files are written by a thread pool: under one process as each batch's rows are ready
+    # (overlapping the engine), under torchrun by rank 0 after the gather
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(dist_mod.usable_cpus()) as writers:
+        pending = []
+        for (names, (h, w)), counts, boxes, scores, labels in model.run_batches(tagged, raw=True):
+            for name, rows in zip(names, fmt.format_batch(boxes, scores, labels, counts, h, w, opts.dataset)):
+                results[name] = rows
+                if world == 1:
+                    pending.append(writers.submit(fmt.save_npy, opts.save_dir, name, rows))
+        clock.append(("engine", time.perf_counter()))
+        if world > 1:
+            results = dist_mod.gather_rows(results, my_names, img_names, rank, world, shards=shard_names)
+            if rank == 0:
+                pending = [writers.submit(fmt.save_npy, opts.save_dir, name, results[name]) for name in img_names]
+        for f in pending:
+            f.result()  # re-raise a failed write
+    clock.append(("files", time.perf_counter()))
+    if os.environ.get("EDGEDET_DETECT_TIMING") == "1":
+        print("detect timing (s): " + ", ".join(f"{k} {b - a:.3f}" for (_, a), (k, b) in zip(clock, clock[1:])) +
+              f", images {len(my_names)}", file=sys.stderr, flush=True)
     return results if rank == 0 else None
 
 

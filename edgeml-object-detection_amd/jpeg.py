@@ -27,30 +27,44 @@ class Packets(list):
         self.hw = tuple(hw)
 
 
-def packet(data):
-    """Entropy-decode one JPEG file's bytes -> (packet np.uint8 array, (H, W)); (None, reason) when
-    the device path does not handle the file; raises EdgeDetError on corrupt data."""
+def packet(data, pinned=False):
+    """Entropy-decode one JPEG file's bytes -> (packet, (H, W)); (None, reason) when the device path
+    does not handle the file; raises EdgeDetError on corrupt data.  The packet is an np.uint8 array,
+    or with pinned=True a pinned torch uint8 tensor (from torch's caching host allocator, so a
+    batch's packets upload without a staging copy)."""
     L = ops.lib()
     buf = np.frombuffer(data, dtype=np.uint8)
     hw = (ctypes.c_int32 * 2)()
-    # first call sizes the packet; the decode runs twice only when the guess is too small
-    cap = max(4096, 6 * buf.size + 65536)
-    out = np.empty(cap, np.uint8)
-    n = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, out.ctypes.data, cap, hw)
+    # one decode into a buffer of a generous guess; a second only when the guess is too small
+    cap = max(4096, 8 * buf.size + 65536)
+
+    def alloc(k):
+        if pinned:
+            t = torch.empty(k, dtype=torch.uint8, pin_memory=True)
+            return t, t.data_ptr()
+        a = np.empty(k, np.uint8)
+        return a, a.ctypes.data
+
+    out, ptr = alloc(cap)
+    n = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, ptr, cap, hw)
     if n == 0:
         return None, L.edgedet_last_error().decode()
     if n < 0:
         ops.check(int(n))
     if n > cap:
-        out = np.empty(int(n), np.uint8)
-        m = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, out.ctypes.data, int(n), hw)
+        out, ptr = alloc(int(n))
+        m = L.edgedet_jpeg_packet(buf.ctypes.data, buf.size, ptr, int(n), hw)
         if m != n:
             ops.check(int(m) if m < 0 else -1)
     return out[:int(n)], (int(hw[0]), int(hw[1]))
 
 
+def _nbytes(p):
+    return int(p.numel()) if torch.is_tensor(p) else int(p.size)
+
+
 def plane_bytes(pk):
-    return int(ops.lib().edgedet_jpeg_plane_bytes(pk.ctypes.data))
+    return int(ops.lib().edgedet_jpeg_plane_bytes(pk.data_ptr() if torch.is_tensor(pk) else pk.ctypes.data))
 
 
 def reconstruct_host(pk, hw):
@@ -78,9 +92,11 @@ class BatchDecoder:
         B, C, H, W = out.shape
         if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(packets) != B:
             raise ValueError("decode: out must be a contiguous cuda uint8 [B,3,H,W] tensor, one packet per image")
-        # one upload: [offsets int64, padded to 256 B][packet 0][packet 1]... (each 256-B aligned)
+        # device image: [offsets int64, padded to 256 B][packet 0][packet 1]... (each 256-B aligned);
+        # numpy packets go through one pinned staging copy, pinned tensor packets are uploaded as they are
         head = (8 * B + 255) // 256 * 256
-        sizes = [int(p.size) for p in packets]
+        sizes = [_nbytes(p) for p in packets]
+        direct = all(torch.is_tensor(p) and p.is_pinned() for p in packets)
         offs = np.zeros(B, np.int64)
         offs[1:] = np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])[:-1]
         offs += head
@@ -89,19 +105,24 @@ class BatchDecoder:
         stride = (max(blocks) * 64 + 255) // 256 * 256
         if self.done is not None:
             self.done.synchronize()  # the previous batch's upload has left the staging buffer
-        if self.stage.numel() < total:
-            self.stage = torch.empty(total * 2, dtype=torch.uint8).pin_memory()
+        staged = head if direct else total
+        if self.stage.numel() < staged:
+            self.stage = torch.empty(staged * 2, dtype=torch.uint8).pin_memory()
         if self.dev.numel() < total:
             self.dev = torch.empty(total * 2, dtype=torch.uint8, device=self.device)
         if self.planes.numel() < B * stride:
             self.planes = torch.empty(B * stride * 2, dtype=torch.uint8, device=self.device)
         st = self.stage.numpy()
         st[:8 * B] = offs.view(np.uint8)
-        for p, o in zip(packets, offs):
-            st[o:o + p.size] = p
+        if not direct:
+            for p, o, n in zip(packets, offs, sizes):
+                st[o:o + n] = p.numpy() if torch.is_tensor(p) else p
         s = stream or torch.cuda.current_stream(self.device)
         with torch.cuda.stream(s):
-            self.dev[:total].copy_(self.stage[:total], non_blocking=True)
+            self.dev[:staged].copy_(self.stage[:staged], non_blocking=True)
+            if direct:  # the caching host allocator keeps each packet's block until its copy is done
+                for p, o, n in zip(packets, offs, sizes):
+                    self.dev[int(o):int(o) + n].copy_(p, non_blocking=True)
             base = self.dev.data_ptr()
             ops.check(ops.lib().edgedet_jpeg_decode_batch(ctypes.c_void_p(base), ctypes.c_void_p(base), B, H, W,
                                                            max(blocks), ctypes.c_void_p(self.planes.data_ptr()),

@@ -359,6 +359,10 @@ int edgedet_output_features(const double* rows, const int64_t* off, int64_t n_im
  * edgedet_jpeg_reconstruct_host is the same reconstruction on the host (test checker).
  */
 int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* out, int64_t cap, int32_t* hw);
+/* (H, W) of n image files from their headers (JPEG SOFn, PNG IHDR; what PIL's Image.open(path).size
+ * reports, the shapes read_image returns), parsed on `threads` host threads (0 = all): hw[2i], hw[2i+1];
+ * (0, 0) for a file whose header was not understood (the caller falls back).  Returns the count found. */
+int64_t edgedet_image_dims(const char* const* paths, int64_t n, int32_t* hw, int32_t threads);
 int64_t edgedet_jpeg_plane_bytes(const void* host_packet);
 int edgedet_jpeg_decode_batch(const void* packets, const int64_t* offsets, int32_t B, int32_t H, int32_t W,
                               int32_t max_blocks, void* planes, int64_t plane_stride, uint8_t* out, void* stream);

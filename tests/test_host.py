@@ -159,7 +159,7 @@ def test_ssd_plan_lowering():
     # blocks 0.2 and 0.3 (no SE, <= 32 channels in and out) as single MBCONV ops: one depthwise and
     # two convs fewer each
     mb = kinds.count(ops.MBCONV)
-    assert mb == (2 if os.environ.get("EDGEDET_MB_BLOCK") == "1" else 0)
+    assert mb == (0 if os.environ.get("EDGEDET_MB_BLOCK") == "0" else 2)
     # the head branches of maps 1..5 as one SSD_HEADS op per branch (10 depthwise + 10 convs fewer)
     grouped = os.environ.get("EDGEDET_SSD_HEADS") == "1"
     assert kinds.count(ops.SSD_HEADS) == (2 if grouped else 0)

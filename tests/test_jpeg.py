@@ -87,3 +87,40 @@ def test_packets_of_the_synthetic_dataset(tmp_path):
         data = (tmp_path / (n + ".jpg")).read_bytes()
         pk, hw = jpeg.packet(data)
         np.testing.assert_array_equal(jpeg.reconstruct_host(pk, hw), _ref(data))
+
+
+def test_image_dims_match_pil_headers(tmp_path):
+    """edgedet_image_dims (the detect CLI's batch sizing, csrc/jpeg.hip) against PIL's Image.open(path).size
+    over baseline / progressive / grayscale JPEGs, one with an EXIF block holding a JPEG thumbnail, PNG,
+    and files it must leave to the caller (BMP, not an image, missing)."""
+    import ctypes
+    from edgeml_amd import detect, ops
+    rs = np.random.RandomState(3)
+    paths = []
+    for k, (h, w) in enumerate([(480, 640), (37, 1001), (1, 1), (640, 427)]):
+        im = Image.fromarray(rs.randint(0, 255, (h, w, 3), dtype=np.uint8))
+        p = tmp_path / f"b{k}.jpg"
+        im.save(p, quality=85)
+        paths.append(p)
+    im = Image.fromarray(rs.randint(0, 255, (300, 200, 3), dtype=np.uint8))
+    im.save(tmp_path / "prog.jpg", progressive=True)
+    im.convert("L").save(tmp_path / "gray.jpg")
+    thumb = io.BytesIO()
+    Image.fromarray(rs.randint(0, 255, (64, 96, 3), dtype=np.uint8)).save(thumb, "JPEG")
+    exif = Image.Exif()
+    exif[0x0112] = 6  # orientation (not applied by read_image nor by PIL's size)
+    big = Image.fromarray(rs.randint(0, 255, (123, 456, 3), dtype=np.uint8))
+    big.save(tmp_path / "exif.jpg", exif=exif.tobytes() + b"\0" * 16 + thumb.getvalue())
+    im.save(tmp_path / "img.png")
+    im.save(tmp_path / "img.bmp")
+    (tmp_path / "text.jpg").write_bytes(b"not an image at all")
+    paths += [tmp_path / n for n in ("prog.jpg", "gray.jpg", "exif.jpg", "img.png", "img.bmp", "text.jpg", "missing.jpg")]
+    hw = np.full((len(paths), 2), -1, np.int32)
+    arr = (ctypes.c_char_p * len(paths))(*[bytes(str(p), "utf-8") for p in paths])
+    found = ops.lib().edgedet_image_dims(ctypes.cast(arr, ctypes.c_void_p), len(paths), hw.ctypes.data, 2)
+    assert found == len(paths) - 3
+    for p, (h, w) in zip(paths, hw):
+        if p.suffix == ".bmp" or p.name in ("text.jpg", "missing.jpg"):
+            assert (h, w) == (0, 0), p
+        else:
+            assert (h, w) == detect._image_size(str(p)), p

@@ -163,13 +163,15 @@ def test_pack_rejects_bad_state_dict(built):
 
 
 def test_fused_block_lowering(built, monkeypatch):
-    """The opt-in whole-block MBCONV lowering (EDGEDET_MB_BLOCK=1) replaces blocks 0.2 and 0.3."""
+    """The whole-block MBCONV lowering (default; EDGEDET_MB_BLOCK=0 turns it off) replaces blocks 0.2
+    and 0.3."""
     _, m = built("ssd")
-    monkeypatch.setenv("EDGEDET_MB_BLOCK", "1")
     B, H, W = 5, 300, 400  # a shape no other test lowers (the library caches plans per shape)
-    native.release("ssd", B, H, W)
-    P = m.build_plan(B, H, W)
-    assert sum(op.kind == ops.MBCONV for op in P.ops) == 2
+    for v, n in (("1", 2), ("0", 0)):
+        monkeypatch.setenv("EDGEDET_MB_BLOCK", v)
+        native.release("ssd", B, H, W)
+        P = m.build_plan(B, H, W)
+        assert sum(op.kind == ops.MBCONV for op in P.ops) == n
     native.release("ssd", B, H, W)
 
 
