@@ -64,16 +64,27 @@ def test_ssd_packing_matches_restatement(built, rt):
     sd, m = built("ssd", 91 if rt else 21, rt)
     P = m.build_plan(2, 320, 320)
     s = lambda k: _np(sd[k])  # noqa: E731
-    p = "backbone.features.0.2.block.0"  # expand 1x1 + BN (eps 1e-3)
-    w, b = fold_bn(s(p + ".0.weight"), s(p + ".1.weight"), s(p + ".1.bias"), s(p + ".1.running_mean"),
-                   s(p + ".1.running_var"), 1e-3)
-    _check_conv(m, _op(P, p), w, b)
-    p = "backbone.features.0.2.block.1"  # depthwise, tap-major
-    w, b = fold_bn(s(p + ".0.weight"), s(p + ".1.weight"), s(p + ".1.bias"), s(p + ".1.running_mean"),
-                   s(p + ".1.running_var"), 1e-3)
+    fb = lambda p: fold_bn(s(p + ".0.weight"), s(p + ".1.weight"), s(p + ".1.bias"),  # noqa: E731
+                           s(p + ".1.running_mean"), s(p + ".1.running_var"), 1e-3)
+    p = "backbone.features.0.4.block.0"  # expand 1x1 + BN (eps 1e-3)
+    _check_conv(m, _op(P, p), *fb(p))
+    p = "backbone.features.0.4.block.1"  # depthwise, tap-major
+    w, b = fb(p)
     op = _op(P, p)
     np.testing.assert_array_equal(_blob_f32(m, op.p[1], w.size), pack_dw_weight(w).reshape(-1))
     np.testing.assert_array_equal(_blob_f32(m, op.p[2], b.size), b)
+    # block 0.2 as one MBCONV record: expand [Cexp][i12], depthwise tap-major, project [Cout][i13]
+    p = "backbone.features.0.2.block"
+    op = _op(P, p)
+    assert op.kind == ops.MBCONV
+    (w1, b1), (wd, bd), (w2, b2) = fb(p + ".0"), fb(p + ".1"), fb(p + ".2")
+    for (w, b), kw, kb, kld in (((w1, b1), 1, 2, 12), ((w2, b2), 5, 6, 13)):
+        wp, _, Kpad, _ = pack_conv_weight(w)
+        assert op.i[kld] == Kpad
+        np.testing.assert_array_equal(_blob_f32(m, op.p[kw], wp.size), wp.reshape(-1))
+        np.testing.assert_array_equal(_blob_f32(m, op.p[kb], b.size), b)
+    np.testing.assert_array_equal(_blob_f32(m, op.p[3], wd.size), pack_dw_weight(wd).reshape(-1))
+    np.testing.assert_array_equal(_blob_f32(m, op.p[4], bd.size), bd)
     p = "head.classification_head.module_list.0.1"  # 1x1 with bias, no BN
     _check_conv(m, _op(P, p), s(p + ".weight").astype(np.float32), s(p + ".bias"))
     p = "backbone.features.0.4.block.2"  # SqueezeExcitation: fc1 [S][C], fc2 transposed [S][C]
