@@ -300,18 +300,35 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
 //   2. stem outputs on the 18 x 18 halo (zero outside the map: the depthwise pads them), one pixel x
 //      16 channels per thread, taps in the packed (kh, kw, ci) order;
 //   3. per output pixel: depthwise (taps (kh, kw) as dw_group), projection, + bias, + residual.
-// The weights are wave-uniform scalar loads.
+// The weights (1024 floats) are staged in LDS with the input tile, in the same memory round trip, and
+// read as wave-wide broadcasts (as scalar loads they did not fit the SGPRs and were re-fetched per
+// pixel: the kernel waited on the scalar cache for half its lifetime).
 constexpr int STEM_T = 16, STEM_SH = STEM_T + 2, STEM_XH = 2 * STEM_SH + 1, STEM_SS = 20;
+// LDS weight image: w0 [16][36] (taps (kh, kw, ci)), b0 [16], wd [9][16], bd [16], w1 [16][16], b1 [16]
+constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 = 752, STEM_B1 = 1008, STEM_NW = 1024;
 
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
+    __shared__ __attribute__((aligned(16))) float ws[STEM_NW];
     const int tid = threadIdx.x, b = blockIdx.y;
     const int oh0 = (blockIdx.x / tiles_w) * STEM_T, ow0 = (blockIdx.x % tiles_w) * STEM_T;
     const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
     const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
     const float* xb = p.x + (int64_t)b * p.H * p.W * 4;
-    {  // all of a thread's input pixels in flight at once (one memory round trip)
+    {  // all of a thread's input pixels and weights in flight at once (one memory round trip)
+        float wv[STEM_NW / 256];
+#pragma unroll
+        for (int r = 0; r < STEM_NW / 256; ++r) {
+            const int e = tid + 256 * r;
+            const float* src = e < STEM_B0   ? p.w0 + (e / 36) * p.ld0 + e % 36
+                               : e < STEM_WD ? p.b0 + (e - STEM_B0)
+                               : e < STEM_BD ? p.wd + (e - STEM_WD)
+                               : e < STEM_W1 ? p.bd + (e - STEM_BD)
+                               : e < STEM_B1 ? p.w1 + ((e - STEM_W1) / 16) * p.ld1 + (e - STEM_W1) % 16
+                                             : p.b1 + (e - STEM_B1);
+            wv[r] = *src;
+        }
         constexpr int R = (STEM_XH * STEM_XH + 255) / 256;
         f32x4 xv[R];
 #pragma unroll
@@ -326,9 +343,12 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (tid + 256 * r < STEM_XH * STEM_XH) *reinterpret_cast<f32x4*>(xs + 4 * (tid + 256 * r)) = xv[r];
+#pragma unroll
+        for (int r = 0; r < STEM_NW / 256; ++r) ws[tid + 256 * r] = wv[r];
     }
     __syncthreads();
     for (int v = tid; v < STEM_SH * STEM_SH; v += 256) {
+        asm volatile("" ::: "memory");  // keep the weight reads in the loop (hoisted, they took 256 VGPRs)
         const int lh = v / STEM_SH, lw = v % STEM_SH;
         const bool in = (unsigned)(sh0 + lh) < (unsigned)p.Ho && (unsigned)(sw0 + lw) < (unsigned)p.Wo;
         f32x4 xt[9];
@@ -338,7 +358,7 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
         float* d = ss + v * STEM_SS;
 #pragma unroll
         for (int co = 0; co < 16; ++co) {
-            const float* w = p.w0 + co * p.ld0;
+            const float* w = ws + STEM_W0 + co * 36;
             float acc = 0.f;
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
@@ -347,7 +367,7 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
                 acc = fmaf(w[4 * t + 2], xt[t].z, acc);
                 acc = fmaf(w[4 * t + 3], xt[t].w, acc);
             }
-            d[co] = in ? apply_act(acc + p.b0[co], ACT_HSWISH) : 0.f;
+            d[co] = in ? apply_act(acc + ws[STEM_B0 + co], ACT_HSWISH) : 0.f;
         }
     }
     __syncthreads();
@@ -363,22 +383,22 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
             const float* sv = ss + ((lh + kh) * STEM_SH + lw + kw) * STEM_SS;
-            const float* wv = p.wd + (kh * 3 + kw) * 16;
+            const float* wv = ws + STEM_WD + (kh * 3 + kw) * 16;
 #pragma unroll
             for (int c = 0; c < 16; ++c) dv[c] = fmaf(sv[c], wv[c], dv[c]);
         }
     }
 #pragma unroll
-    for (int c = 0; c < 16; ++c) dv[c] = apply_act(dv[c] + p.bd[c], ACT_RELU);
+    for (int c = 0; c < 16; ++c) dv[c] = apply_act(dv[c] + ws[STEM_BD + c], ACT_RELU);
     const float* res = ss + ((lh + 1) * STEM_SH + lw + 1) * STEM_SS;
     float out[16];
 #pragma unroll
     for (int co = 0; co < 16; ++co) {
-        const float* w = p.w1 + co * p.ld1;
+        const float* w = ws + STEM_W1 + co * 16;
         float acc = 0.f;
 #pragma unroll
         for (int ci = 0; ci < 16; ++ci) acc = fmaf(w[ci], dv[ci], acc);
-        out[co] = (acc + p.b1[co]) + res[co];
+        out[co] = (acc + ws[STEM_B1 + co]) + res[co];
     }
     float* yp = p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow) * 16;
 #pragma unroll
