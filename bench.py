@@ -247,6 +247,10 @@ def op_work(op):
             fl += 2.0 * B * H * W * C * (9 + 6 * cols)
             by += 4.0 * (B * H * W * C + 10 * C + 6 * cols * (C + 1) + B * H * W * 6 * cols)
         return "ssd_heads", fl, by
+    if k == O.MBCONV:  # expand 1x1 + depthwise KxK + project 1x1 (+ residual): block input in, output out
+        B, H, W, Cin, Cexp, Cout, Ho, Wo, K = (i[j] for j in range(9))
+        fl = 2.0 * B * (H * W * Cin * Cexp + Ho * Wo * Cexp * (K * K + Cout))
+        return "mbconv", fl, 4.0 * (B * H * W * Cin + B * Ho * Wo * Cout + Cexp * (Cin + K * K + Cout + 2) + Cout)
     if k in (O.FORK, O.JOIN, O.WAIT):
         return "lanes", 0.0, 0.0
     if k == O.MEMSET:  # zeroing the output of a split-K conv
@@ -406,12 +410,26 @@ def orie_vs_ref(n=48, E=None):
                     with open(d("labels", name[:-4] + ".txt"), "w") as f:
                         for r in rows[rows[:, 5] >= 0.3]:
                             f.write(" ".join([str(int(r[0]))] + [repr(float(v)) for v in r[1:5]]) + "\n")
+        # where the ORIE difference comes from: per detector, the images whose files differ
+        # in structure (row count or label sequence: a boundary flip or a reordering), and the largest
+        # value difference over the structurally equal files (fp32 summation order)
+        files = {}
+        for tag in ("weak", "strong"):
+            structural, max_val = 0, 0.0
+            for i in range(n):
+                a, b = (np.load(d(side + "_" + tag, f"{i:012d}.npy")) for side in ("eng", "ref"))
+                if a.shape != b.shape or not np.array_equal(a[:, 0], b[:, 0]):
+                    structural += 1
+                elif len(a):
+                    max_val = max(max_val, float(np.abs(a - b).max()))
+            files[tag] = {"structural": structural, "max_value_diff": max_val}
         wd, sd, lab = reward.set_data(d("eng_weak"), d("eng_strong"), d("labels"))
         got = reward.compute_orie_all(wd, sd, lab, E, seed=1000)
         want = orie.orie_all(d("ref_weak"), d("ref_strong"), d("labels"), E, seed=1000)
     d = np.abs(got - want)
     out = {"max_abs_diff": float(d.max()), "images": n, "num_ensemble": E,
-           "images_differing": int(np.count_nonzero(d)), "nonzero_ref": int(np.count_nonzero(want))}
+           "images_differing": int(np.count_nonzero(d)), "nonzero_ref": int(np.count_nonzero(want)),
+           "files": files}
     frcnn_cpu = {"value": round((n - 1) / cpu_s["strong"], 3), "unit": "images/s", "cores": torch.get_num_threads(),
                  "kind": "port", "host_cores": os.cpu_count(), "host_cpu": _cpu_model(),
                  "sample": f"{n - 1} synthetic 640x640 images, batch=1 ({cpu_s['strong']:.1f}s), frcnn CPU oracle "
