@@ -62,6 +62,7 @@
 #include <string>
 
 #include <map>
+#include <set>
 #include <utility>
 
 #include "kernels.hpp"
@@ -597,6 +598,10 @@ struct Graph {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 };
+// Live graphs: launch and destroy refuse a handle that is not one (a destroyed or foreign pointer
+// would otherwise reach hipGraphLaunch and crash the host process).
+static std::mutex g_graphs_mu;
+static std::set<Graph*> g_graphs;
 
 }  // namespace edgedet
 
@@ -659,13 +664,20 @@ extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stre
         set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e2));
         return -2;
     }
+    {
+        std::lock_guard<std::mutex> lock(g_graphs_mu);
+        g_graphs.insert(g);
+    }
     *out = g;
     return 0;
 }
 
 extern "C" int edgedet_graph_launch(void* graph, void* stream) {
     Graph* g = reinterpret_cast<Graph*>(graph);
-    EDGEDET_REQUIRE(g && g->exec, "graph_launch: null graph");
+    {
+        std::lock_guard<std::mutex> lock(g_graphs_mu);
+        EDGEDET_REQUIRE(g && g_graphs.count(g) && g->exec, "graph_launch: not a live graph (null or destroyed)");
+    }
     EDGEDET_CHECK_HIP(hipGraphLaunch(g->exec, (hipStream_t)stream));
     return 0;
 }
@@ -673,6 +685,10 @@ extern "C" int edgedet_graph_launch(void* graph, void* stream) {
 extern "C" int edgedet_graph_destroy(void* graph) {
     Graph* g = reinterpret_cast<Graph*>(graph);
     if (!g) return 0;
+    {
+        std::lock_guard<std::mutex> lock(g_graphs_mu);
+        EDGEDET_REQUIRE(g_graphs.erase(g) == 1, "graph_destroy: not a live graph (destroyed twice?)");
+    }
     if (g->exec) (void)hipGraphExecDestroy(g->exec);
     if (g->graph) (void)hipGraphDestroy(g->graph);
     delete g;

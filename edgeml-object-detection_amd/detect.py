@@ -111,56 +111,45 @@ def image_sizes(dataset, workers=None):
     return sizes
 
 
-def _packet_or_none(path):
-    """The device-decode packet of a JPEG file (csrc/jpeg.hip; entropy decode on this host thread, the
-    GIL released inside the library), or None when the file is not a JPEG the device path handles."""
-    from . import jpeg
-    with open(path, "rb") as f:
-        data = f.read()
-    if data[:2] != b"\xff\xd8":
-        return None
-    pk, _ = jpeg.packet(data, pinned=torch.cuda.is_available())
-    return pk
-
-
 def _decoded_batches(dataset, chunks, sizes, workers=None, device_decode=True):
     """Yield (names, (H, W), batch) for the given batches of equal-size images (lists of dataset
-    indices, distributed.size_batches).  With device_decode, a batch whose files are all JPEGs the
-    device decoder handles is a jpeg.Packets (entropy-decoded on the host threads, reconstructed on
-    the GPU by run_batches straight into the plan's input, byte-identical to the host decode);
-    otherwise the images are decoded on the host straight into their slots of a pinned uint8 batch
-    buffer.  One thread per usable host core (PIL and the library release the GIL while decoding), the
-    next two batches in flight while the caller uses the current one."""
+    indices, distributed.size_batches).  With device_decode, a batch of JPEG files the device decoder
+    handles is entropy-decoded by one library call on all usable host cores into one pinned buffer
+    (jpeg.PackedBatch; reconstructed on the GPU by run_batches straight into the plan's input,
+    byte-identical to the host decode); otherwise (another format, or a JPEG the device path does not
+    take) the images are decoded on the host (PIL, one thread per usable core) straight into their
+    slots of a pinned uint8 batch buffer.  The next two batches are in flight while the caller uses the
+    current one."""
     import concurrent.futures as cf
     from . import jpeg
     from .distributed import usable_cpus
     workers = workers or usable_cpus()
     paths = [os.path.join(dataset.img_dir, n) for n in dataset.img_names]
-    with cf.ThreadPoolExecutor(workers) as ex:
-        pin = torch.cuda.is_available()
+    pin = torch.cuda.is_available()
+    # packed batches one after another on one thread (each call uses every core); host decodes per image
+    with cf.ThreadPoolExecutor(1) as packer, cf.ThreadPoolExecutor(workers) as ex:
 
         def host(c):
             h, w = sizes[c[0]]
             buf = torch.empty((len(c), 3, h, w), dtype=torch.uint8, pin_memory=pin)
             return "host", buf, [ex.submit(dataset.read_u8, i, buf[k]) for k, i in enumerate(c)]
 
-        def sub(c):  # one future per image, so a batch decodes on many threads at once
-            if device_decode:
-                return "pk", None, [ex.submit(_packet_or_none, paths[i]) for i in c]
+        def sub(c):
+            if device_decode and all(paths[i][-4:].lower() in (".jpg", "jpeg", ".jpe") for i in c):
+                return "pk", None, [packer.submit(jpeg.batch_packets, [paths[i] for i in c], workers, pin)]
             return host(c)
 
         fut = [sub(c) for c in chunks[:2]]
         for j, c in enumerate(chunks):
             kind, buf, fs = fut[j]
             res = [f.result() for f in fs]
-            if kind == "pk" and any(r is None for r in res):  # a file the device path does not take
+            if kind == "pk" and res[0] is None:  # a file the device path does not take
                 kind, buf, fs = host(c)
                 res = [f.result() for f in fs]
             if j + 2 < len(chunks):
                 fut.append(sub(chunks[j + 2]))
             fut[j] = None
-            batch = jpeg.Packets(res, sizes[c[0]]) if kind == "pk" else buf
-            yield [dataset.img_names[i] for i in c], sizes[c[0]], batch
+            yield [dataset.img_names[i] for i in c], sizes[c[0]], (res[0] if kind == "pk" else buf)
 
 
 def detect_rows(model, images, dataset="coco"):
@@ -228,7 +217,8 @@ def main(opts):
     clock.append(("files", time.perf_counter()))
     if os.environ.get("EDGEDET_DETECT_TIMING") == "1":
         print("detect timing (s): " + ", ".join(f"{k} {b - a:.3f}" for (_, a), (k, b) in zip(clock, clock[1:])) +
-              f", images {len(my_names)}", file=sys.stderr, flush=True)
+              f", images {len(my_names)}; engine phases (s): " +
+              ", ".join(f"{k} {v:.3f}" for k, v in getattr(model, "phase_s", {}).items()), file=sys.stderr, flush=True)
     return results if rank == 0 else None
 
 

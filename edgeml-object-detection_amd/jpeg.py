@@ -59,6 +59,52 @@ def packet(data, pinned=False):
     return out[:int(n)], (int(hw[0]), int(hw[1]))
 
 
+class PackedBatch:
+    """One batch of equal-size JPEG files entropy-decoded by edgedet_jpeg_batch_packets into a single
+    pinned buffer laid out as the device image edgedet_jpeg_decode_batch reads (offset table, then the
+    packets): uploaded with one copy, reconstructed on the device by run_batches into the plan's
+    input."""
+
+    def __init__(self, buf, span, hw, plane_bytes, n):
+        self.buf, self.span, self.hw, self.plane_bytes, self.n = buf, int(span), tuple(hw), int(plane_bytes), int(n)
+
+    def __len__(self):
+        return self.n
+
+
+def batch_packets(paths, threads=0, pinned=True):
+    """Entropy-decode a batch of JPEG files of one size on `threads` host threads in one library call
+    -> PackedBatch, or None when a file is not a JPEG the device path handles or the sizes differ (the
+    caller decodes the batch on the host).  Raises EdgeDetError on unreadable / corrupt files."""
+    import os
+    L = ops.lib()
+    n = len(paths)
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    hw = np.zeros((n, 2), np.int32)
+    planes = ctypes.c_int64(0)
+    # the packets run a few times the file bytes; a second call only when this guess is too small
+    def size(p):
+        try:
+            return os.path.getsize(p)
+        except OSError:  # the library reports the unreadable file
+            return 0
+    cap = (8 * n + 255) // 256 * 256 + sum((8 * size(p) + 65536 + 255) // 256 * 256 for p in paths)
+    for _ in range(2):
+        buf = torch.empty(cap, dtype=torch.uint8, pin_memory=pinned)
+        span = L.edgedet_jpeg_batch_packets(ctypes.cast(arr, ctypes.c_void_p), n, buf.data_ptr(), cap,
+                                            hw.ctypes.data, ctypes.byref(planes), int(threads))
+        if span == 0:
+            return None
+        if span < 0:
+            ops.check(int(span))
+        if span <= cap:
+            if (hw != hw[0]).any():
+                return None
+            return PackedBatch(buf, span, hw[0], planes.value, n)
+        cap = int(span)
+    raise ops.EdgeDetError("jpeg_batch_packets: packet sizes changed between two decodes of the same files")
+
+
 def _nbytes(p):
     return int(p.numel()) if torch.is_tensor(p) else int(p.size)
 
@@ -89,6 +135,8 @@ class BatchDecoder:
         self.done = None
 
     def decode(self, packets, out, stream=None):
+        if isinstance(packets, PackedBatch):
+            return self.decode_packed(packets, out, stream)
         B, C, H, W = out.shape
         if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(packets) != B:
             raise ValueError("decode: out must be a contiguous cuda uint8 [B,3,H,W] tensor, one packet per image")
@@ -130,4 +178,26 @@ class BatchDecoder:
                                                            ops.stream_handle(s)))
             self.done = torch.cuda.Event()
             self.done.record(s)
+        return out
+
+    def decode_packed(self, pb, out, stream=None):
+        """A PackedBatch: one H2D copy of its span, then the device reconstruction into out.  The
+        caching host allocator keeps pb.buf's block until the copy has run."""
+        B, C, H, W = out.shape
+        if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(pb) != B or \
+                pb.hw != (H, W):
+            raise ValueError("decode: out must be a contiguous cuda uint8 [B,3,H,W] tensor of the batch's size")
+        if self.dev.numel() < pb.span:
+            self.dev = torch.empty(pb.span * 2, dtype=torch.uint8, device=self.device)
+        stride = (pb.plane_bytes + 255) // 256 * 256
+        if self.planes.numel() < B * stride:
+            self.planes = torch.empty(B * stride * 2, dtype=torch.uint8, device=self.device)
+        s = stream or torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            self.dev[:pb.span].copy_(pb.buf[:pb.span], non_blocking=True)
+            base = self.dev.data_ptr()
+            ops.check(ops.lib().edgedet_jpeg_decode_batch(ctypes.c_void_p(base), ctypes.c_void_p(base), B, H, W,
+                                                           pb.plane_bytes // 64, ctypes.c_void_p(self.planes.data_ptr()),
+                                                           stride, ctypes.c_void_p(out.data_ptr()),
+                                                           ops.stream_handle(s)))
         return out

@@ -17,6 +17,8 @@ missing).  Architecture and post-processing constants: SURVEY.md Appendix A.
 import math
 
 import numpy as np
+import time
+
 import torch
 
 from . import arch
@@ -159,6 +161,18 @@ class _Detector:
             del slots[key]
         pending = []  # (tag, slot, B)
         turn = [0]
+        # host seconds per phase (EDGEDET_DETECT_TIMING: the detect CLI prints them): waiting for the
+        # caller's next batch (its decode), building + capturing slot plans, issuing a batch (upload /
+        # device decode, replay, D2H), waiting for a batch's results
+        tm = self.__dict__.setdefault("phase_s", {})
+        for k in ("input", "plans", "issue", "results", "caller"):
+            tm.setdefault(k, 0.0)
+        clk = [time.perf_counter()]
+
+        def lap(k):
+            t = time.perf_counter()
+            tm[k] += t - clk[0]
+            clk[0] = t
 
         def new_slot(key, first):
             B, H, W, u8 = key
@@ -179,7 +193,9 @@ class _Detector:
             return slots[key][turn[0] % n]
 
         def collect(tag, sl, B):
+            lap("issue")
             sl["done"].synchronize()
+            lap("results")
             sl["src"] = None
             if raw:
                 return tag, sl["count"].numpy().copy(), sl["box"].numpy().copy(), sl["score"].numpy().copy(), \
@@ -189,10 +205,17 @@ class _Detector:
             return tag, [(box[j, :counts[j]].copy(), score[j, :counts[j]].copy(), label[j, :counts[j]].copy())
                          for j in range(B)]
 
-        from .jpeg import BatchDecoder, Packets
+        def emit(item):
+            r = collect(*item)
+            lap("results")
+            yield r
+            lap("caller")  # the caller's work on the rows (formatting, file writes)
+
+        from .jpeg import BatchDecoder, PackedBatch, Packets
         for tag, imgs in batches:
+            lap("input")
             whole = imgs if torch.is_tensor(imgs) and imgs.dim() == 4 else None
-            if isinstance(imgs, Packets):  # JPEG packets: decoded on the device into the plan's input
+            if isinstance(imgs, (Packets, PackedBatch)):  # JPEG packets: decoded on the device into the plan's input
                 shapes, dtypes, B = {imgs.hw}, {torch.uint8}, len(imgs)
             elif whole is not None:
                 shapes, dtypes, B = {tuple(whole.shape[-2:])}, {whole.dtype}, whole.shape[0]
@@ -207,18 +230,20 @@ class _Detector:
                 # a new shape: finish the old shape's batches and free its plans (the CLI groups
                 # images by size, so a real image set touches each shape in one run of batches)
                 while pending:
-                    yield collect(*pending.pop(0))
+                    yield from emit(pending.pop(0))
                 for k in slots:
                     self.plans.pop(k, None)
                 slots.clear()
+            lap("issue")
             sl = slot(key)
+            lap("plans")
             # the slot's previous batch (if any) must be on the host before its buffers are reused
             while any(p is sl for _, p, _ in pending):
-                yield collect(*pending.pop(0))
+                yield from emit(pending.pop(0))
             plan, stream = sl["plan"], sl["stream"]
             stage = sl["stage"]
             sl["done"].synchronize()  # a slot left in flight by an abandoned earlier call
-            if isinstance(imgs, Packets):
+            if isinstance(imgs, (Packets, PackedBatch)):
                 src = None
             elif whole is not None and whole.dtype in (torch.uint8, torch.float32) and whole.is_contiguous() and \
                     (whole.is_pinned() or whole.device == self.device):
@@ -231,10 +256,12 @@ class _Detector:
                 for j, im in enumerate(whole if whole is not None else imgs):
                     stage[j].copy_(im if key[3] else im.to(torch.float32))
                 src = stage
+            lap("issue")
             if plan.graph is None:
                 # one hipGraph per slot plan (captured on first use): a batch is then one launch
                 # instead of a host call per op, which kept the host, not the device, the bottleneck
                 plan.capture(stream)
+            lap("plans")
             with torch.cuda.stream(stream):
                 if src is None:
                     if sl["jpeg"] is None:
@@ -250,9 +277,10 @@ class _Detector:
                 sl["done"].record(stream)
             pending.append((tag, sl, B))
             while len(pending) >= n:
-                yield collect(*pending.pop(0))
+                yield from emit(pending.pop(0))
         while pending:
-            yield collect(*pending.pop(0))
+            yield from emit(pending.pop(0))
+        lap("issue")
 
 
 

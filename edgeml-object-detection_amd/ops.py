@@ -55,7 +55,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_model_records", "edgedet_ssdlite_workspace_size", "edgedet_ssdlite_forward",
            "edgedet_frcnn_workspace_size", "edgedet_frcnn_forward", "edgedet_plan_check", "edgedet_release_lanes",
            "edgedet_lane_sets", "edgedet_nms_workspace_size", "edgedet_nms_ws", "edgedet_batched_nms_ws",
-           "edgedet_topk_segments", "edgedet_box_decode", "edgedet_jpeg_packet", "edgedet_jpeg_plane_bytes", "edgedet_image_dims",
+           "edgedet_topk_segments", "edgedet_box_decode", "edgedet_jpeg_packet", "edgedet_jpeg_batch_packets", "edgedet_jpeg_plane_bytes", "edgedet_image_dims",
            "edgedet_jpeg_decode_batch", "edgedet_jpeg_reconstruct_host", "edgedet_model_buffers", "edgedet_model_op_names", "edgedet_model_release")
 
 
@@ -99,6 +99,8 @@ def lib():
     L.edgedet_batched_nms_ws.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp, _i64, _vp]
     L.edgedet_jpeg_packet.argtypes = [_vp, _i64, _vp, _i64, _vp]
     L.edgedet_jpeg_packet.restype = _i64
+    L.edgedet_jpeg_batch_packets.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, _i32]
+    L.edgedet_jpeg_batch_packets.restype = _i64
     L.edgedet_jpeg_plane_bytes.argtypes = [_vp]
     L.edgedet_image_dims.argtypes = [_vp, _i64, _vp, _i32]
     L.edgedet_image_dims.restype = _i64

@@ -352,16 +352,19 @@ class NativeBuf:
     """A named carve-out of a NativePlan's workspace (edgedet_model_buffers)."""
 
     def __init__(self, plan, name, offset, nbytes, dtype, shape):
-        self.plan, self.name, self.off, self.nbytes = plan, name, int(offset), int(nbytes)
+        # the workspace tensor, not the plan: no plan <-> buffer reference cycle, so a plan (its graph
+        # and workspace) is released when its last user drops it, at a known point, never by a
+        # garbage-collector pass on whatever thread triggers one (possibly while graphs are launching)
+        self.arena, self.name, self.off, self.nbytes = plan.arena, name, int(offset), int(nbytes)
         self.dtype, self.shape = dtype, tuple(int(v) for v in shape)
 
     def ptr(self):
-        return self.plan.arena.data_ptr() + self.off
+        return self.arena.data_ptr() + self.off
 
     def tensor(self):
         es = _esize(self.dtype)
         n = int(np.prod(self.shape))
-        return self.plan.arena[self.off:self.off + n * es].view(self.dtype).view(self.shape)
+        return self.arena[self.off:self.off + n * es].view(self.dtype).view(self.shape)
 
 
 class NativePlan:

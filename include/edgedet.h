@@ -359,6 +359,15 @@ int edgedet_output_features(const double* rows, const int64_t* off, int64_t n_im
  * edgedet_jpeg_reconstruct_host is the same reconstruction on the host (test checker).
  */
 int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* out, int64_t cap, int32_t* hw);
+/* A batch of n JPEG files entropy-decoded on `threads` host threads (0 = all) straight into the device
+ * image edgedet_jpeg_decode_batch reads (offsets = packets = out once uploaded): out[0..8n) the int64
+ * packet offsets (padded to 256 B), then the 256-B aligned packets; hw[2i..2i+1] = (H, W) of file i,
+ * *max_plane_bytes = the largest plane_bytes of the batch.  Returns the span to upload; a span above
+ * cap means nothing usable was written (retry with that many bytes).  0 = a file the device path does
+ * not handle (decode the batch on the host), < 0 = unreadable or corrupt file.  The detect CLI's image
+ * read (detect.py:55-58) for one batch in one call. */
+int64_t edgedet_jpeg_batch_packets(const char* const* paths, int64_t n, void* out, int64_t cap, int32_t* hw,
+                                   int64_t* max_plane_bytes, int32_t threads);
 /* (H, W) of n image files from their headers (JPEG SOFn, PNG IHDR; what PIL's Image.open(path).size
  * reports, the shapes read_image returns), parsed on `threads` host threads (0 = all): hw[2i], hw[2i+1];
  * (0, 0) for a file whose header was not understood (the caller falls back).  Returns the count found. */

@@ -124,3 +124,52 @@ def test_image_dims_match_pil_headers(tmp_path):
             assert (h, w) == (0, 0), p
         else:
             assert (h, w) == detect._image_size(str(p)), p
+
+
+def test_batch_packets_equal_per_file_packets(tmp_path):
+    """edgedet_jpeg_batch_packets (the detect CLI's one-call batch entropy decode) lays out exactly the
+    per-file packets of edgedet_jpeg_packet behind its offset table, for several thread counts, with a
+    first guess too small (the retry path); unsupported and corrupt files come back as None / an error."""
+    from edgeml_amd import ops
+    rs = np.random.RandomState(4)
+    paths = []
+    for k in range(7):
+        p = tmp_path / f"{k}.jpg"
+        p.write_bytes(_encode(_scene(96, 128, 10 + k), quality=int(rs.randint(40, 100)),
+                              subsampling=int(rs.randint(0, 3))))
+        paths.append(str(p))
+    want = [jpeg.packet(open(p, "rb").read())[0] for p in paths]
+    for threads in (1, 3, 0):
+        pb = jpeg.batch_packets(paths, threads, pinned=False)
+        assert pb.hw == (96, 128) and len(pb) == len(paths)
+        buf = pb.buf.numpy()
+        offs = buf[:8 * len(paths)].view(np.int64)
+        assert (offs % 256 == 0).all() and pb.span <= buf.size
+        for o, w in zip(offs, want):
+            np.testing.assert_array_equal(buf[o:o + w.size], w)
+        assert pb.plane_bytes == max(jpeg.plane_bytes(w) for w in want)
+    # a buffer too small: the call reports the span it needs and writes nothing past cap
+    import ctypes
+    arr = (ctypes.c_char_p * 3)(*[p.encode() for p in paths[:3]])
+    hw, planes = np.zeros((3, 2), np.int32), ctypes.c_int64(0)
+    small = np.full(300, 7, np.uint8)
+    need = ops.lib().edgedet_jpeg_batch_packets(ctypes.cast(arr, ctypes.c_void_p), 3, small.ctypes.data, 256,
+                                                hw.ctypes.data, ctypes.byref(planes), 2)
+    assert need > 256 and (small[256:] == 7).all()
+    full = np.zeros(need, np.uint8)
+    assert ops.lib().edgedet_jpeg_batch_packets(ctypes.cast(arr, ctypes.c_void_p), 3, full.ctypes.data, need,
+                                                hw.ctypes.data, ctypes.byref(planes), 2) == need
+    for o, w in zip(full[:24].view(np.int64), want[:3]):
+        np.testing.assert_array_equal(full[o:o + w.size], w)
+    prog = tmp_path / "prog.jpg"
+    prog.write_bytes(_encode(_scene(96, 128, 1), progressive=True))
+    assert jpeg.batch_packets(paths[:2] + [str(prog)], 2, pinned=False) is None
+    other = tmp_path / "other.jpg"
+    other.write_bytes(_encode(_scene(64, 128, 1)))
+    assert jpeg.batch_packets(paths[:2] + [str(other)], 2, pinned=False) is None  # sizes differ
+    bad = tmp_path / "bad.jpg"
+    bad.write_bytes(b"\xff\xd8\xff\xdb" + bytes(40))
+    with pytest.raises(ops.EdgeDetError):
+        jpeg.batch_packets(paths[:2] + [str(bad)], 2, pinned=False)
+    with pytest.raises(ops.EdgeDetError):
+        jpeg.batch_packets([str(tmp_path / "missing.jpg")], 1, pinned=False)
