@@ -3,7 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model ssd|frcnn|both] [--no-cpu]
 
 A step = one forward of the detector over one batch of synthetic 640x640 images already resident in
-HBM (preprocess -> backbone -> heads -> decode -> NMS -> final top-k), replayed from a captured
+HBM as the decoded uint8 images the detect CLI hands the engine (read_image's output, detect.py:57; the
+/255 of detect.py:58 runs in the device transform, bit-identical to the host's float path; --input f32
+keeps the model contract's float images instead) (/255 -> preprocess -> backbone -> heads -> decode ->
+NMS -> final top-k), replayed from a captured
 hipGraph, plus the D2H copy of the batch's detections (counts, boxes, scores, labels) into pinned
 host memory.  The steps rotate over the model's INFLIGHT independent plan instances
 (SSDLite 4, FRCNN 2: the counts the detect CLI's run_batches keeps on the device); the SSD rate at
@@ -129,13 +132,20 @@ def end_to_end(m, B, batches, seed):
                     "(no JPEG decode, no file write)"}
 
 
-def inflight_instances(m, B, n, seed):
-    """n-1 more independent plans of the same (model, B, 640, 640), inputs filled like the first."""
+def fill_input(plan, B, seed):
+    """The plan's input batch: the decoded uint8 images (u8 plans: read_image's output, detect.py:57,
+    divided by 255 in the device transform) or the model contract's float images."""
     from edgeml_amd import synthetic
+    src = synthetic.make_batch_u8(B, 640, 640, seed=seed) if plan.u8 else synthetic.make_batch(B, 640, 640, seed=seed)
+    plan.input.tensor().copy_(src.cuda())
+
+
+def inflight_instances(m, B, n, seed, u8=True):
+    """n-1 more independent plans of the same (model, B, 640, 640), inputs filled like the first."""
     out = []
     for k in range(1, n):
-        p = m.build_plan(B, 640, 640).finalize()
-        p.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=seed + k).cuda())
+        p = m.build_plan(B, 640, 640, u8).finalize()
+        fill_input(p, B, seed + k)
         s = torch.cuda.Stream()
         p.capture(s)
         out.append((p, s))
@@ -482,7 +492,12 @@ def main():
     ap.add_argument("--dump-ops", default="", help="write the per-op device times of each model to this JSON")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host uint8 -> rows) rates")
     ap.add_argument("--e2e-batches", type=int, default=40)
+    ap.add_argument("--input", default="u8", choices=["u8", "f32"],
+                    help="what the step's input batch in HBM holds: the decoded uint8 images (the detect CLI's "
+                         "engine input; /255 in the device transform, bit-identical to the host's float path) "
+                         "or the model contract's float images")
     args = ap.parse_args()
+    u8 = args.input == "u8"
 
     dist, rank, world = dist_setup(args.gpus)
     from edgeml_amd import models, synthetic
@@ -492,21 +507,23 @@ def main():
     if args.model in ("ssd", "both", "all"):
         B = args.ssd_batch
         m = models.ssdlite320_mobilenet_v3_large().to("cuda")
-        plan = m.plan(B, 640, 640)
-        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank).cuda())
+        plan = m.plan(B, 640, 640, u8)
+        fill_input(plan, B, 100 * rank)
         plan.capture(stream)
         nin = args.inflight or m.INFLIGHT
-        extra = inflight_instances(m, B, nin, 100 * rank)
+        extra = inflight_instances(m, B, nin, 100 * rank, u8)
         el = timed_steps(plan, stream, args.steps, args.warmup, dist, extra)
         out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
                       "inflight": nin, "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
-        # SURVEY §8(d)'s binding roof for C2: 87.1 MB of algorithmic HBM traffic per image
-        gbs = SSD_BYTES_PER_IMG * out["ssd"]["value"] / world / 1e9
-        out["ssd"]["step_hbm"] = {"bytes_per_img": SSD_BYTES_PER_IMG, "achieved_GBps": round(gbs, 1),
+        # SURVEY §8(d)'s binding roof for C2: 87.1 MB of algorithmic HBM traffic per image with the fp32
+        # input image (4.92 MB); a uint8 input batch reads 1.23 MB of it instead
+        bpi = SSD_BYTES_PER_IMG - (3 * 640 * 640 * 3 if u8 else 0)
+        gbs = bpi * out["ssd"]["value"] / world / 1e9
+        out["ssd"]["step_hbm"] = {"bytes_per_img": bpi, "achieved_GBps": round(gbs, 1),
                                   "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4)}
         if not args.no_alt:  # the other in-flight count, same plans (reported beside the headline)
             alt = 2 if nin != 2 else 4
-            more = inflight_instances(m, B, alt - nin + 1, 100 * rank + 7) if alt > nin else []
+            more = inflight_instances(m, B, alt - nin + 1, 100 * rank + 7, u8) if alt > nin else []
             el2 = timed_steps(plan, stream, args.steps, args.warmup, dist, (extra + more)[:alt - 1])
             del more
             out["ssd"]["alt_inflight"] = {"inflight": alt, "value": round(world * B * args.steps / el2, 2)}
@@ -523,11 +540,11 @@ def main():
     if args.model in ("retinanet", "all"):
         B = args.retina_batch
         m = models.retinanet_resnet50_fpn_v2().to("cuda")
-        plan = m.plan(B, 640, 640)
-        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 70).cuda())
+        plan = m.plan(B, 640, 640, u8)
+        fill_input(plan, B, 100 * rank + 70)
         plan.capture(stream)
         steps = max(20, args.steps // 10)
-        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 70)
+        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 70, u8)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
         out["retinanet"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
@@ -538,10 +555,10 @@ def main():
     if args.model in ("frcnn", "both", "all"):
         B = args.frcnn_batch
         m = models.fasterrcnn_resnet50_fpn_v2().to("cuda")
-        plan = m.plan(B, 640, 640)
-        plan.input.tensor().copy_(synthetic.make_batch(B, 640, 640, seed=100 * rank + 50).cuda())
+        plan = m.plan(B, 640, 640, u8)
+        fill_input(plan, B, 100 * rank + 50)
         plan.capture(stream)
-        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 50)
+        extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 50, u8)
         steps = max(20, args.steps // 10)  # FRCNN steps are ~20x SSD's: at least 20 (about half a second)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         del extra
@@ -578,6 +595,8 @@ def main():
                                 "retinanet": "retinanet_resnet50_fpn_v2 b=%d 640x640"}[primary] % p["batch"],
                    "global_batch": p["batch"] * world, "parallelism": f"dp{world}",
                    "batches_in_flight": p.get("inflight", args.inflight),
+                   "input": ("uint8 decoded images in HBM (read_image, detect.py:57); /255 in the device transform"
+                             if u8 else "float32 images in HBM (the model contract, detect.py:58)"),
                    "conv_math": plan_mod.CONV_MATH,
                    "weights": "seeded synthetic (COCO weights need a download)"},
     }

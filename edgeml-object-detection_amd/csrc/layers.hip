@@ -8,6 +8,11 @@
 //   maxpool      ResNet stem max_pool2d(3,2,1); FPN LastLevelMaxPool(1,2,0) App. A.2 steps 2-3
 //   roi_align    MultiScaleRoIAlign: LevelMapper + roi_align(7x7, sr=2, aligned=False)
 //                                                                          App. A.2 step 5, row a13
+#include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "kernels.hpp"
 
 namespace edgedet {
@@ -443,239 +448,288 @@ extern "C" int edgedet_ssd_stem(const float* x, int64_t B, int64_t H, int64_t W,
 // A whole torchvision InvertedResidual without SqueezeExcitation (SSDLite blocks
 // 0.2 / 0.3 at 160^2 / 80^2): expand 1x1 (+ folded BN, act), depthwise KxK stride S (+ folded BN, act),
 // project 1x1 (+ folded BN), + the block input when S == 1 and Cin == Cout.  Neither the 3-4x-wide
-// expanded tensor nor the depthwise output reaches HBM.  Block = one image, an 8 x 8 output tile,
-// 8 waves; the expanded channels are processed in chunks of 32 through LDS:
-//   expand   v_mfma_f32_32x32x2_f32 (exact fp32 products): [halo pixels, 32-row tiles over the waves]
-//            x [Cin] x [32 channels]; + bias, act; halo pixels outside the image are zero (the
-//            depthwise conv pads the expanded tensor with zeros);
-//   depthwise VALU from LDS, taps in (kh, kw) order, + bias, act;
-//   project  v_mfma_f32_32x32x2_f32: [64 output pixels] x [32 chunk channels] x [Cout], accumulated in
-//            registers over the chunks (waves own (pixel tile, K quarter) pairs).
-// The round-2 form (expansion and projection on the VALU, one pixel x channel per thread) measured
-// 3.5-4.5x slower than the three separate ops; the matrix-core form keeps each phase to a few MFMAs
-// per wave.
-constexpr int MBF_T = 8, MBF_CC = 32;
-typedef float mbf_floatx16 __attribute__((ext_vector_type(16)));
+// expanded tensor nor the depthwise output reaches HBM.
+// Block = one image's TH x TW output tile (8 x 8 at stride 1, 4 x 8 at stride 2); one wave per 16
+// expanded channels (Cexp <= 128: up to 8 waves).  The input halo is staged in LDS once (the only
+// barrier before the final reduction); after it each wave runs its own chunk start to end with no
+// workgroup barrier — the round-2 / early round-3 forms shared 32-channel chunks between the waves and
+// paid four barriers per chunk, and measured at 15-20 TFLOP/s with half the wave time waiting:
+//   expand   v_mfma_f32_16x16x4_f32 (exact fp32): [halo pixels] x [Cin] x [the wave's 16 channels],
+//            two independent accumulation chains at a time; + bias, act; halo pixels outside the image
+//            are zero (the depthwise conv pads the expanded tensor with zeros); into the wave's LDS;
+//   depthwise lane = (channel, row group), a K x K register window slid along the row (3 or 6 new
+//            LDS reads per output instead of 9), taps in (kh, kw) order, + bias, act; into LDS;
+//   project  v_mfma_f32_16x16x4_f32: [tile pixels] x [the wave's 16 channels] x [Cout <= 32];
+// then the waves' partial projections are added in wave order ((w0 + w1) + w2 ...), + bias (+ the
+// input pixel), and stored.  All weights live in registers, loaded before the halo.
+constexpr int MBW_C = 16;    // expanded channels per wave
+constexpr int MBW_MAXW = 8;  // waves per workgroup (Cexp <= 128)
 
-template <int K, int S, int CINP>
-struct MbfGeom {
-    static constexpr int IH = (MBF_T - 1) * S + K, NPX = IH * IH, NPXP = (NPX + 31) / 32 * 32;
-    static constexpr int XS = CINP + 1;    // odd row pitch: conflict-free column reads
-    static constexpr int ES = MBF_CC + 1;  // expanded chunk row pitch
+template <int K, int S, int CINP, int TH, int TW>
+struct MbwGeom {
+    static constexpr int IHh = (TH - 1) * S + K, IWh = (TW - 1) * S + K;  // halo rows, columns
+    static constexpr int NPX = IHh * IWh, NPXP = (NPX + 15) / 16 * 16;
+    static constexpr int P = TH * TW;                                       // output pixels (16k)
+    static constexpr int XS = CINP + 1;                                     // odd pitches: spread banks
+    static constexpr int ES = MBW_C + 1;
+    static constexpr int PS = 33;                                           // partial sums: 32 + 1
+    static constexpr int EW = NPXP * ES > P * PS ? NPXP * ES : P * PS;      // per wave: chunk, then partials
+    static size_t smem(int nw) { return 4 * ((size_t)NPXP * (XS + 1) + (size_t)nw * (EW + P * ES)); }
 };
 
-// NCO: 32-wide Cout tiles (Cout <= 32 * NCO; the launcher instantiates NCO = 1).  8 waves (16 per CU
-// at two workgroups, to cover the halo and weight loads).  A chunk's weights (expand rows, project
-// columns, depthwise taps, biases) are loaded into registers one chunk ahead, all loads of a thread
-// issued together, and stored to LDS at the chunk boundary; the projection's two 32-pixel tiles are
-// split over the eight waves by K quarter (wave w: tile w & 1, channels 8 (w >> 1) .. + 7 of each
-// chunk), and the quarters are added once at the end in a fixed order ((q0 + q2) + (q1 + q3)).
-template <int K, int S, int ACT, int CINP, int NCO>
-__global__ void __launch_bounds__(512) mbconv_kernel(MbParams p, int tiles_w) {
-    static_assert(NCO == 1, "mbconv: the K-split projection is laid out for one Cout tile");
-    using G = MbfGeom<K, S, CINP>;
-    constexpr int IH = G::IH, NPX = G::NPX, NPXP = G::NPXP, XS = G::XS, ES = G::ES, TT = MBF_T * MBF_T;
-    __shared__ float xs[NPXP * XS];        // input halo [pixel][Cin] (rows past NPX zero)
-    __shared__ float es[NPXP * ES];        // expanded chunk [halo pixel][32]; at the end the K-quarter partials
-    __shared__ float ds[TT * ES];          // depthwise chunk [output pixel][32]
-    __shared__ float w1s[MBF_CC * XS];     // expand weights of the chunk [32][Cin]
-    __shared__ float w2s[32 * NCO * ES];   // project weights of the chunk [Cout pad][32]
-    __shared__ float wds[K * K * MBF_CC];  // depthwise taps of the chunk [tap][32]
-    __shared__ float b1s[MBF_CC], bds[MBF_CC];
-    static_assert(4 * 64 * 16 <= NPXP * ES, "two K-quarter partial pairs fit the expanded-chunk buffer");
-    constexpr int NT = 512, NW = NT / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, h = lane >> 5;
-    const int b = blockIdx.y;
-    const int oh0 = (blockIdx.x / tiles_w) * MBF_T, ow0 = (blockIdx.x % tiles_w) * MBF_T;
-    const int ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
+__device__ __forceinline__ void mbw_wave_sync() {  // this wave's LDS writes visible to its own lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int K, int S, int ACT, int CINP, int TH, int TW>
+__global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, int tiles_w, int tiles_img, int ntiles, int diag) {
+    using G = MbwGeom<K, S, CINP, TH, TW>;
+    constexpr int IWh = G::IWh, NPX = G::NPX, NPXP = G::NPXP, P = G::P;
+    constexpr int XS = G::XS, ES = G::ES, PS = G::PS, EW = G::EW;
+    constexpr int NT = NPXP / 16, KS = CINP / 4, PT = P / 16, Q4 = CINP / 4;
+    constexpr int HR = (NPXP * Q4 + 255) / 256;  // halo float4s per thread (at least four waves)
+    static_assert(P % 16 == 0 && TW % 4 == 0 && NPXP <= 256, "mbconv: tile shape");
+    extern __shared__ __attribute__((aligned(16))) float mb_smem[];
+    const int nt = (int)blockDim.x, nw = nt >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15, q = lane >> 4;
+    float* xs = mb_smem;                                        // [NPXP][XS] input halo
+    float* es = mb_smem + NPXP * XS + wid * EW;                 // [NPXP][ES] expanded chunk; later [P][PS]
+    float* ds = mb_smem + NPXP * XS + nw * EW + wid * P * ES;   // [P][ES] depthwise outputs
+    float* xm = mb_smem + NPXP * XS + nw * (EW + P * ES);       // [NPXP] 1 inside the image, else 0
     const int Cin = p.Cin, Cexp = p.Cexp, Cout = p.Cout;
-    const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
-    // chunk operands in registers (zero past Cexp / Cin / Cout)
-    constexpr int N1 = MBF_CC * CINP, N2 = 32 * NCO * MBF_CC, ND = K * K * MBF_CC + 2 * MBF_CC;
-    constexpr int U1 = (N1 + NT - 1) / NT, U2 = (N2 + NT - 1) / NT, UD = (ND + NT - 1) / NT;
-    float r1[U1], r2[U2], rd[UD];
-    auto load_chunk = [&](int c0) {
+    const int ch = wid * MBW_C + l16;  // this lane's expanded channel
+    const bool chv = ch < Cexp;
+    // weights in registers for the workgroup's lifetime; every load issued unconditionally (a clamped
+    // index, the value masked) so they are all in flight together
+    float w1r[KS], w2r[4][2], wdr[K * K];
+    const int chc = chv ? ch : 0;
 #pragma unroll
-        for (int u = 0; u < U1; ++u) {
-            const int t = tid + NT * u, n = t / CINP, c = t - n * CINP;
-            r1[u] = (t < N1 && c0 + n < Cexp && c < Cin) ? p.w1[(int64_t)(c0 + n) * p.ld1 + c] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U2; ++u) {
-            const int t = tid + NT * u, co = t / MBF_CC, j = t - co * MBF_CC;
-            r2[u] = (t < N2 && co < Cout && c0 + j < Cexp) ? p.w2[(int64_t)co * p.ld2 + c0 + j] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < UD; ++u) {
-            const int t = tid + NT * u;
-            float v = 0.f;
-            if (t < K * K * MBF_CC) {
-                const int tap = t / MBF_CC, j = t - tap * MBF_CC;
-                v = c0 + j < Cexp ? p.wd[(int64_t)tap * Cexp + c0 + j] : 0.f;
-            } else if (t < K * K * MBF_CC + MBF_CC) {
-                const int j = t - K * K * MBF_CC;
-                v = c0 + j < Cexp ? p.b1[c0 + j] : 0.f;
-            } else if (t < ND) {
-                const int j = t - K * K * MBF_CC - MBF_CC;
-                v = c0 + j < Cexp ? p.bd[c0 + j] : 0.f;
-            }
-            rd[u] = v;
-        }
-    };
-    auto store_chunk = [&]() {
-#pragma unroll
-        for (int u = 0; u < U1; ++u) {
-            const int t = tid + NT * u, n = t / CINP, c = t - n * CINP;
-            if (t < N1) w1s[n * XS + c] = r1[u];
-        }
-#pragma unroll
-        for (int u = 0; u < U2; ++u) {
-            const int t = tid + NT * u, co = t / MBF_CC, j = t - co * MBF_CC;
-            if (t < N2) w2s[co * ES + j] = r2[u];
-        }
-#pragma unroll
-        for (int u = 0; u < UD; ++u) {
-            const int t = tid + NT * u;
-            if (t < K * K * MBF_CC) wds[t] = rd[u];
-            else if (t < K * K * MBF_CC + MBF_CC) b1s[t - K * K * MBF_CC] = rd[u];
-            else if (t < ND) bds[t - K * K * MBF_CC - MBF_CC] = rd[u];
-        }
-    };
-    load_chunk(0);
-    // 1. input halo (zero outside the image and past Cin), all loads of a thread in flight together
-    {
-        constexpr int N = NPXP * CINP, U = (N + NT - 1) / NT;
-        float v[U];
-#pragma unroll
-        for (int r = 0; r < U; ++r) {
-            const int t = tid + NT * r;
-            const int px = t / CINP, c = t - px * CINP;
-            const int ih = ih0 + px / IH, iw = iw0 + px % IH;
-            const bool in = t < N && px < NPX && c < Cin && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            v[r] = in ? xb[((int64_t)ih * p.W + iw) * Cin + c] : 0.f;
-        }
-#pragma unroll
-        for (int r = 0; r < U; ++r) {
-            const int t = tid + NT * r;
-            if (t < N) xs[(t / CINP) * XS + t % CINP] = v[r];
-        }
+    for (int s = 0; s < KS; ++s) {
+        const bool ok = chv && 4 * s + q < Cin;
+        const float v = p.w1[(int64_t)chc * p.ld1 + (ok ? 4 * s + q : 0)];
+        w1r[s] = ok ? v : 0.f;
     }
-    mbf_floatx16 acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int pt = wid & 1, kq = wid >> 1, kh0 = 8 * kq;  // projection: pixel tile, K quarter of the chunk
-    for (int c0 = 0; c0 < Cexp; c0 += MBF_CC) {
-        __syncthreads();  // xs written; the previous chunk's es / ds / weights consumed
-        store_chunk();
-        if (c0 + MBF_CC < Cexp) load_chunk(c0 + MBF_CC);  // in flight under this chunk's three phases
-        __syncthreads();
-        // 2. expand: wave w takes 32-pixel row tiles w, w + 8, ...
-        for (int t = wid; t < NPXP / 32; t += NW) {
-            mbf_floatx16 e;
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) e[r] = 0.f;
-            const float* ar = xs + (32 * t + l32) * XS + h;
-            const float* br = w1s + l32 * XS + h;
+        for (int n = 0; n < 2; ++n) {
+            const int co = 16 * n + l16, k = wid * MBW_C + 4 * s + q;
+            const bool ok = co < Cout && k < Cexp;
+            const float v = p.w2[ok ? (int64_t)co * p.ld2 + k : 0];
+            w2r[s][n] = ok ? v : 0.f;
+        }
 #pragma unroll
-            for (int k = 0; k < CINP; k += 2) e = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], e, 0, 0, 0);
-            const float bias = b1s[l32];
+    for (int t = 0; t < K * K; ++t) {
+        const float v = p.wd[(int64_t)t * Cexp + chc];
+        wdr[t] = chv ? v : 0.f;
+    }
+    const float b1 = chv ? p.b1[chc] : 0.f, bd = chv ? p.bd[chc] : 0.f;
+    // the halo of a tile: [NPX][Cin] as 16-byte loads (Cin % 4 == 0), zero outside the image / past Cin;
+    // the next tile's halo is in flight in registers while the current tile is computed.  A thread's
+    // halo slots (pixel row / column, channel quad) are the same for every tile: decomposed once.
+    f32x4 hv[HR];
+    int hr[HR], hc[HR], hoff[HR], hdst[HR];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int ih = ih0 + m / IH, iw = iw0 + m % IH;
-                const bool in = m < NPX && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-                es[m * ES + l32] = in ? apply_act(e[r] + bias, ACT) : 0.f;
+    for (int u = 0; u < HR; ++u) {
+        const int t = tid + nt * u, px = t / Q4, c4 = t - px * Q4;
+        const bool live = t < NPXP * Q4 && px < NPX && 4 * c4 < Cin;
+        hr[u] = live ? px / IWh : -(1 << 20);  // a dead slot never passes the bounds test
+        hc[u] = px % IWh;
+        hoff[u] = 4 * c4;
+        hdst[u] = t < NPXP * Q4 ? px * XS + 4 * c4 : -1;
+    }
+    const int mr = tid < NPXP ? tid / IWh : 0, mc = tid % IWh;  // this thread's mask pixel (tid < NPXP)
+    auto load_halo = [&](int tile) {
+        const int b = tile / tiles_img, r = tile - b * tiles_img, th = r / tiles_w, tw = r - th * tiles_w;
+        const int ih0 = th * TH * S - p.pad, iw0 = tw * TW * S - p.pad;
+        const float* xb = p.x + (int64_t)b * p.H * p.W * Cin;
+#pragma unroll
+        for (int u = 0; u < HR; ++u) {
+            const int ih = ih0 + hr[u], iw = iw0 + hc[u];
+            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            if (diag & 2) {
+                hv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                continue;
+            }
+            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + (ok ? (ih * p.W + iw) * Cin + hoff[u] : 0));
+            hv[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile < ntiles) load_halo(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int b = tile / tiles_img, r = tile - b * tiles_img, th = r / tiles_w, tw = r - th * tiles_w;
+        const int oh0 = th * TH, ow0 = tw * TW, ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
+        __syncthreads();  // the previous tile's reads of xs and of the partials are done
+#pragma unroll
+        for (int u = 0; u < HR; ++u) {
+            if (hdst[u] >= 0) {
+                float* d = xs + hdst[u];
+                d[0] = hv[u].x;
+                d[1] = hv[u].y;
+                d[2] = hv[u].z;
+                d[3] = hv[u].w;
             }
         }
+        if (tid < NPXP) {  // NPXP <= 4 waves of threads (the launcher's minimum)
+            const int ih = ih0 + mr, iw = iw0 + mc;
+            xm[tid] = tid < NPX && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W ? 1.f : 0.f;
+        }
+        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);
         __syncthreads();
-        // 3. depthwise: thread = (channel tid & 31, output pixels (tid >> 5) + 16 j)
-        {
-            const int ch = tid & 31;
-            float wt[K * K];
+        // expand: the wave's 16 channels over every halo pixel, two accumulation chains at a time
+        // (x 0 outside the image: the depthwise conv zero-pads the expanded tensor)
+        auto expand_store = [&](const f32x4& a, int t) {
 #pragma unroll
-            for (int q = 0; q < K * K; ++q) wt[q] = wds[q * MBF_CC + ch];
-            const float bd = bds[ch];
+            for (int i = 0; i < 4; ++i) {
+                const int m = 16 * t + 4 * q + i;
+                es[m * ES + l16] = apply_act(a[i] + b1, ACT) * xm[m];
+            }
+        };
+#pragma unroll 1
+        for (int t = 0; t < (diag & 8 ? 0 : NT); t += 2) {
+            f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+            const float* r0 = xs + (16 * t + l16) * XS + q;
 #pragma unroll
-            for (int j = 0; j < TT / 16; ++j) {
-                const int op = (tid >> 5) + 16 * j;
-                const int ly = op / MBF_T, lx = op % MBF_T;
+            for (int s = 0; s < KS; ++s) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(r0[4 * s], w1r[s], a0, 0, 0, 0);
+                if (t + 1 < NT) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(r0[16 * XS + 4 * s], w1r[s], a1, 0, 0, 0);
+            }
+            expand_store(a0, t);
+            if (t + 1 < NT) expand_store(a1, t + 1);
+        }
+        mbw_wave_sync();
+        // depthwise: lane = (channel l16, output rows q, q + 4, ...), a K x K window slid along the row
+#pragma unroll 1
+        for (int oy = q; oy < (diag & 4 ? 0 : TH); oy += 4) {
+            float win[K][K];
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw) win[kh][kw] = es[((oy * S + kh) * IWh + kw) * ES + l16];
+#pragma unroll
+            for (int ox = 0; ox < TW; ++ox) {
+                if (ox > 0) {
+#pragma unroll
+                    for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+                        for (int kw = 0; kw < K - S; ++kw) win[kh][kw] = win[kh][kw + S];
+#pragma unroll
+                        for (int kw = K - S; kw < K; ++kw)
+                            win[kh][kw] = es[((oy * S + kh) * IWh + ox * S + kw) * ES + l16];
+                    }
+                }
                 float a = 0.f;
 #pragma unroll
                 for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-                    for (int kw = 0; kw < K; ++kw) a = fmaf(es[((ly * S + kh) * IH + lx * S + kw) * ES + ch], wt[kh * K + kw], a);
-                ds[op * ES + ch] = apply_act(a + bd, ACT);
+                    for (int kw = 0; kw < K; ++kw) a = fmaf(win[kh][kw], wdr[kh * K + kw], a);
+                ds[(oy * TW + ox) * ES + l16] = apply_act(a + bd, ACT);
             }
         }
+        mbw_wave_sync();
+        // project the wave's 16 channels: acc[pixel tile][Cout half]
+        f32x4 acc[PT][2];
+#pragma unroll
+        for (int t = 0; t < PT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < PT; ++t) {
+                const float a = ds[(16 * t + l16) * ES + 4 * s + q];
+                acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w2r[s][0], acc[t][0], 0, 0, 0);
+                acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w2r[s][1], acc[t][1], 0, 0, 0);
+            }
+        // the partials replace the expanded chunk in this wave's region (its last reads were above)
+#pragma unroll
+        for (int t = 0; t < PT; ++t)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) es[(16 * t + 4 * q + i) * PS + 16 * n + l16] = acc[t][n][i];
         __syncthreads();
-        // 4. project: wave w = (pixel tile w & 1, K quarter w >> 1) over the Cout tile
-        {
-            const float* ar = ds + (32 * pt + l32) * ES + kh0 + h;
-            const float* br = w2s + l32 * ES + kh0 + h;
-#pragma unroll
-            for (int k = 0; k < MBF_CC / 4; k += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[k], br[k], acc, 0, 0, 0);
+        // partials added in wave order, bias, residual (S == 1: the input pixel at the tap centre), store
+        const float* part = mb_smem + NPXP * XS;
+        for (int e = tid; e < P * 32; e += nt) {
+            const int px = e >> 5, co = e & 31;
+            const int ly = px / TW, lx = px - ly * TW, oh = oh0 + ly, ow = ow0 + lx;
+            if (co >= Cout || oh >= p.Ho || ow >= p.Wo) continue;
+            float v = part[px * PS + co];
+            for (int w = 1; w < nw; ++w) v += part[w * EW + px * PS + co];
+            v += p.b2[co];
+            if (p.residual) v += xs[((ly + p.pad) * IWh + lx + p.pad) * XS + co];
+            if (!(diag & 1)) p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
         }
-    }
-    // 5. the K quarters through LDS (es is free: every wave is past the last depthwise): quarters 2, 3
-    //    into 0, 1, then 1 into 0
-    if (kq >= 2) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) es[((wid - 4) * 16 + r) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (kq < 2) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += es[(wid * 16 + r) * 64 + lane];
-    }
-    __syncthreads();
-    if (kq == 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) es[((wid - 2) * 16 + r) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (kq != 0) return;
-    // 6. bias, residual, store (lane = output channel, registers = output pixels)
-    const int co = l32;
-    if (co >= Cout) return;
-    const float bias = p.b2[co];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int op = 32 * pt + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int ly = op / MBF_T, lx = op % MBF_T, oh = oh0 + ly, ow = ow0 + lx;
-        if (oh >= p.Ho || ow >= p.Wo) continue;
-        float v = (acc[r] + es[(wid * 16 + r) * 64 + lane]) + bias;
-        if (p.residual) v = v + xs[((ly + p.pad) * IH + lx + p.pad) * XS + co];  // S == 1: the input pixel
-        p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
     }
 }
 
-template <int K, int S, int CINP, int NCO>
-static int mbconv_launch_kc(const MbParams& p, hipStream_t s) {
-    const int tiles_w = cdiv(p.Wo, MBF_T);
-    const dim3 grid((unsigned)(cdiv(p.Ho, MBF_T) * tiles_w), (unsigned)p.B);
-    switch (p.act) {
-        case ACT_RELU: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
-        case ACT_RELU6: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_RELU6, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
-        case ACT_HSWISH: hipLaunchKernelGGL((mbconv_kernel<K, S, ACT_HSWISH, CINP, NCO>), grid, dim3(512), 0, s, p, tiles_w); break;
-        default: EDGEDET_REQUIRE(false, "mbconv: activation RE / R6 / HS");
-    }
+static int env_flag_int(const char* k) {
+    const char* e = std::getenv(k);
+    return e ? std::atoi(e) : 0;
+}
+
+// Opt an instantiation into its dynamic LDS once per process (not a stream operation: legal while a
+// graph is being captured).
+template <typename KF>
+static int mbw_set_lds(KF kernel, size_t bytes) {
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, size_t>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& d : done)
+        if (d.first == (const void*)kernel && d.second >= bytes) return 0;
+    EDGEDET_CHECK_HIP(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done.emplace_back((const void*)kernel, bytes);
+    return 0;
+}
+
+template <int K, int S, int ACT, int CINP>
+static int mbconv_launch_t(const MbParams& p, hipStream_t s) {
+    constexpr int TH = S == 1 ? 8 : 4, TW = 8;
+    using G = MbwGeom<K, S, CINP, TH, TW>;
+    // at least four waves (the halo loader's stride); waves past Cexp carry zero weights
+    const int nw = std::max(4, (int)cdiv(p.Cexp, MBW_C)), tiles_w = (int)cdiv(p.Wo, TW);
+    const int tiles_img = (int)cdiv(p.Ho, TH) * tiles_w, ntiles = p.B * tiles_img;
+    const size_t lds = G::smem(nw);
+    EDGEDET_REQUIRE(lds <= 160 * 1024, "mbconv: tile exceeds the LDS");
+    auto kern = mbconv_kernel<K, S, ACT, CINP, TH, TW>;
+    if (int rc = mbw_set_lds(kern, lds)) return rc;
+    // a resident grid (the workgroups that fit the CUs at once) looping over the tiles, each tile's
+    // halo loaded under the previous tile's compute
+    const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+    const int grid = std::min(ntiles, 256 * per_cu);
+    // EDGEDET_MB_DIAG (diagnostic only, wrong results): 1 no output stores, 2 no halo loads, 4 no
+    // depthwise, 8 no expansion
+    static const int diag = env_flag_int("EDGEDET_MB_DIAG");
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * nw), lds, s, p, tiles_w, tiles_img, ntiles, diag);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
 
+template <int K, int S, int ACT>
+static int mbconv_launch_a(const MbParams& p, hipStream_t s) {
+    if (p.Cin <= 16) return mbconv_launch_t<K, S, ACT, 16>(p, s);
+    if (p.Cin <= 24) return mbconv_launch_t<K, S, ACT, 24>(p, s);
+    return mbconv_launch_t<K, S, ACT, 32>(p, s);
+}
+
 template <int K, int S>
 static int mbconv_launch_ks(const MbParams& p, hipStream_t s) {
-    if (p.Cout <= 32) {
-        if (p.Cin <= 16) return mbconv_launch_kc<K, S, 16, 1>(p, s);
-        if (p.Cin <= 24) return mbconv_launch_kc<K, S, 24, 1>(p, s);
-        return mbconv_launch_kc<K, S, 32, 1>(p, s);
+    switch (p.act) {
+        case ACT_RELU: return mbconv_launch_a<K, S, ACT_RELU>(p, s);
+        case ACT_RELU6: return mbconv_launch_a<K, S, ACT_RELU6>(p, s);
+        case ACT_HSWISH: return mbconv_launch_a<K, S, ACT_HSWISH>(p, s);
+        default: EDGEDET_REQUIRE(false, "mbconv: activation RE / R6 / HS");
     }
-    EDGEDET_REQUIRE(false, "mbconv: Cout <= 32");
 }
 
 int mbconv_launch(const MbParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w1 && p.b1 && p.wd && p.bd && p.w2 && p.b2 && p.y, "mbconv: null pointer");
-    EDGEDET_REQUIRE(p.Cin >= 1 && p.Cin <= 32 && p.Cout >= 1 && p.Cout <= 32 && p.Cexp >= 1, "mbconv: Cin, Cout <= 32");
+    EDGEDET_REQUIRE(p.Cin >= 1 && p.Cin <= 32 && p.Cin % 4 == 0 && p.Cout >= 1 && p.Cout <= 32 && p.Cexp >= 1 &&
+                        p.Cexp <= MBW_C * MBW_MAXW,
+                    "mbconv: Cin <= 32 (a multiple of 4), Cout <= 32, Cexp <= 128");
+    EDGEDET_REQUIRE(((uintptr_t)p.x & 15) == 0, "mbconv: input 16-byte aligned");
     EDGEDET_REQUIRE(p.ld1 >= p.Cin && p.ld2 >= p.Cexp, "mbconv: weight row strides");
     EDGEDET_REQUIRE(p.pad == (p.K - 1) / 2 && p.Ho == (p.H + 2 * p.pad - p.K) / p.stride + 1 &&
                     p.Wo == (p.W + 2 * p.pad - p.K) / p.stride + 1, "mbconv: 'same' padding shape");

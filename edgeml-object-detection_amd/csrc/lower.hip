@@ -747,9 +747,9 @@ class SSDLite {
         auto inverted_residual = [&](const Cur& in, const Block& b, const std::string& base) {
             Prefixes pf = block_prefixes(b, base);
             // blocks 0.2 / 0.3 as one MBCONV launch each (EDGEDET_MB_BLOCK=0: the three separate ops);
-            // SSD 27.5k -> 28.4k img/s with the 8-wave kernel (r3g)
+            // SSD 27.5k -> 28.4k img/s with the 8-wave kernel (r3g); one wave per 16 channels since r3n
             if (env_int("EDGEDET_MB_BLOCK", 1) == 1 && !pack_only && !pf.pe.empty() && !b.se && b.cin <= 32 &&
-                b.cout <= 32)
+                b.cin % 4 == 0 && b.cout <= 32 && b.exp <= 128)
                 return mb_block(in, b, pf);
             Cur y = in;
             if (!pf.pe.empty()) y = conv(y, pf.pe, b.exp, 1, 1, b.act);

@@ -362,6 +362,8 @@ def test_conv_bf16x6_is_fp32_grade(shape):
     (3, 80, 80, 24, 72, 24, 3, 1, "RE"),      # block 0.3 (residual)
     (1, 37, 29, 12, 40, 20, 5, 2, "HS"),      # ragged tiles, K = 5, a partial channel chunk
     (2, 9, 11, 32, 96, 32, 5, 1, "R6"),       # residual with the 32-channel bound
+    (1, 20, 24, 8, 128, 8, 3, 1, "RE"),       # eight waves (the 128-channel bound), residual
+    (2, 17, 13, 4, 17, 4, 3, 2, "HS"),        # a one-channel last wave, Cin = 4
 ])
 def test_mbconv_block_matches_torch(B, H, W, Cin, E, Cout, k, s, act):
     """The whole InvertedResidual in one kernel (MBCONV record: expand 1x1 + act, depthwise + act,
