@@ -1172,7 +1172,6 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
     };
     // static priority for waves 4..7, the arbitration losers of a two-waves-per-SIMD block
     // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if (p.young_prio && __builtin_amdgcn_readfirstlane(wid) >= 4) __builtin_amdgcn_s_setprio(1);
     if constexpr (PF != 2) {
         // Skewed pipeline: quadrant (1, 1) of stage k-1 is carried across the barrier in F1, so after
         // the barrier the matrix pipe runs it while stage k's first fragments are read; stage k+1's
@@ -1289,27 +1288,10 @@ static bool x6b_presplit(const ConvParams& p) {
     return p.x3 && p.Cin % BK6B == 0 && p.x_pstride % 4 == 0 && ((uintptr_t)p.x3 & 15) == 0;
 }
 
-// The pointwise specialisation of conv_x6b_kernel (EDGEDET_X6B_P1=0: the general uniform-tap form).
-static bool x6b_p1() {
-    static const bool v = [] {
-        const char* e = std::getenv("EDGEDET_X6B_P1");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-static int x6b_young_prio() {
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_X6B_PRIO");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
 
 template <int BM = 256, int PF = 1, int BN = 128>
 static int launch_x6b(const ConvParams& p0, hipStream_t s) {
     ConvParams p = p0;
-    p.young_prio = x6b_young_prio();
     EDGEDET_REQUIRE(p.w3 && ((uintptr_t)p.w3 & 15) == 0, "conv bf16x6: needs 16-byte aligned split weight planes");
     EDGEDET_REQUIRE(p.Kpad % BK6B == 0, "conv bf16x6: Kpad must be a multiple of 32");
     if (p.ksplit > 1)
@@ -1327,7 +1309,7 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
         EDGEDET_LAUNCH_CHECK();
         return 0;
     }
-    const bool p1 = p.lin_x && p.KH == 1 && p.KW == 1 && p.Cin % 4 == 0 && x6b_p1();
+    const bool p1 = p.lin_x && p.KH == 1 && p.KW == 1 && p.Cin % 4 == 0;
     auto k = p1 ? (xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, true, BN> : conv_x6b_kernel<true, false, false, BM, PF, true, BN>)
                       : (ut ? conv_x6b_kernel<false, true, false, BM, PF, true, BN> : conv_x6b_kernel<false, false, false, BM, PF, true, BN>))
          : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, false, BN> : conv_x6b_kernel<true, false, false, BM, PF, false, BN>)
@@ -1389,12 +1371,8 @@ static int launch_pw_splitk(const ConvParams& p, hipStream_t s) {
 // 33: every column block in one wave (weights of NB x KJ <= 18 chunks in registers); 34: one
 // column block per wave (column groups over the waves), next block prefetched; 35: 34 without the
 // prefetch (more waves per SIMD instead).
-static int pw_stream_max_wg() {  // grid cap (EDGEDET_PWS_WG: A/B of waves per block-walk)
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_PWS_WG");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 256 * 8;
-    }();
-    return v;
+static int pw_stream_max_wg() {  // grid cap: 512 - 4096 workgroups measured alike (profiles/r2j_pws_grid.txt)
+    return 256 * 8;
 }
 
 template <int NB, int KJ, bool PF>
@@ -1451,16 +1429,7 @@ static int launch_cfg(const ConvParams& p, hipStream_t s) {
 
 // Tile choice: the direct pointwise kernel for narrow-K 1x1 layers (HBM-bound, no reuse to stage);
 // otherwise the largest LDS-staged tile that still gives about one workgroup per CU.
-static int big_tile_override() {
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_BIG_TILE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
 static int choose_tile(const ConvParams& p) {
-    if (big_tile_override() && (int64_t)p.M >= 65536 && p.Cout >= 128 && p.Kpad >= 512) return big_tile_override();
     if (p.lin_x && p.Kpad >= 256 && p.Cout <= 96) return p.Cout <= 32 ? 13 : (p.Cout <= 64 ? 14 : 13);
     if (p.lin_x && (p.Kpad <= 128 || p.Cout <= 32)) {
         if (p.Cout <= 32) return 15;

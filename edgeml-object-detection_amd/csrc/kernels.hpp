@@ -25,7 +25,6 @@ struct ConvParams {
     float res_sh, res_sw;  // nearest-upsample scales (in/out) for the residual
     int lin_x, lin_y, lin_res;  // dense-layout fast paths (set by conv_launch)
     int ksplit;                 // 2: K halves accumulated with atomics into a zeroed y (tile 26)
-    int young_prio;             // x6b: s_setprio 1 for the second-dispatched half of the waves (A/B)
     FastDiv div_howo, div_wo, div_cin, div_kw;
 };
 
