@@ -68,7 +68,7 @@ def main():
     pipeline.main(pipeline.getargs([img, lab, work, "--num-ensemble", str(a.num_ensemble)]))
     el = time.perf_counter() - t0
     print(f"config 4 pipeline, {a.n} images, E={a.num_ensemble}: {el:.1f} s end to end "
-          f"({a.n / el:.1f} images/s incl. JPEG decode on the host)", flush=True)
+          f"({a.n / el:.1f} images/s incl. JPEG decode, files and ORIE)", flush=True)
     with np.load(os.path.join(work, "reward", f"orie{a.num_ensemble}.npz")) as z:
         r = z["reward"]
     print(f"ORIE over {len(r)} images: {np.count_nonzero(r)} nonzero, finite {bool(np.all(np.isfinite(r)))}",
