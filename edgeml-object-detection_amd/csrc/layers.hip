@@ -526,6 +526,11 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
         wdr[t] = chv ? v : 0.f;
     }
     const float b1 = chv ? p.b1[chc] : 0.f, bd = chv ? p.bd[chc] : 0.f;
+    // the output channel of this thread in the final sum (the element stride is a multiple of 32), its
+    // bias loaded once: a load in that loop would sit behind the previous iteration's output store
+    // (the compiler cannot prove p.b2 and p.y apart) and cost a memory round trip per element
+    const int co_t = tid & 31;
+    const float b2v = p.b2[co_t < Cout ? co_t : 0];
     // the halo of a tile: [NPX][Cin] as 16-byte loads (Cin % 4 == 0), zero outside the image / past Cin;
     // the next tile's halo is in flight in registers while the current tile is computed.  A thread's
     // halo slots (pixel row / column, channel quad) are the same for every tile: decomposed once.
@@ -658,7 +663,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
             if (co >= Cout || oh >= p.Ho || ow >= p.Wo) continue;
             float v = part[px * PS + co];
             for (int w = 1; w < nw; ++w) v += part[w * EW + px * PS + co];
-            v += p.b2[co];
+            v += b2v;
             if (p.residual) v += xs[((ly + p.pad) * IWh + lx + p.pad) * XS + co];
             if (!(diag & 1)) p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
         }
