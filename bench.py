@@ -211,6 +211,10 @@ def op_work(op):
         return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
     if k == O.SSD_STEM:  # stem conv 3x3 s2 (4 -> 16) + depthwise 3x3 + projection 16 -> 16 + residual
         B, H, W, Ho, Wo = (i[j] for j in range(5))
+        H0, W0 = i[7], i[8]
+        if H0:  # the transform folded in: the source image in (uint8 or float), no NHWC4 intermediate
+            src = B * 3 * H0 * W0 * (1 if op.p.get(9) is not None else 4)
+            return "stem", 2.0 * B * Ho * Wo * 16 * (36 + 9 + 16), float(src) + 4.0 * B * Ho * Wo * 16
         return "stem", 2.0 * B * Ho * Wo * 16 * (36 + 9 + 16), 4.0 * (B * H * W * 4 + B * Ho * Wo * 16)
     if k == O.PREPROCESS:
         B, H, W, Ho, Wo, Hp, Wp = (i[j] for j in range(7))

@@ -407,6 +407,14 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.Wo = (int)I[4];
             p.ld0 = (int)I[5];
             p.ld1 = (int)I[6];
+            p.src = P<const float>(o, 8);  // the transform folded in: source image, its size and normalisation
+            p.src8 = P<const uint8_t>(o, 9);
+            p.H0 = (int)I[7];
+            p.W0 = (int)I[8];
+            for (int c = 0; c < 3; ++c) {
+                p.mean[c] = o.f[c];
+                p.stdv[c] = o.f[3 + c];
+            }
             return ssd_stem_launch(p, s);
         }
         case EDGEDET_OP_RETINA_CLASS_NMS: {

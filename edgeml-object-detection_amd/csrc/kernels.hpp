@@ -205,6 +205,13 @@ struct StemParams {
     const float* b1;
     float* y;         // [B][Ho][Wo][16]
     int B, H, W, Ho, Wo, ld0, ld1;
+    // the transform folded in (x unused): the source image [B][3][H0][W0], float or uint8 (/ 255), its
+    // normalisation, resized to H x W (scales set by the launcher)
+    const float* src;
+    const uint8_t* src8;
+    int H0, W0;
+    float mean[3], stdv[3];
+    float sh, sw;
 };
 int ssd_stem_launch(const StemParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);

@@ -29,6 +29,35 @@ __device__ __forceinline__ float pre_load(const T* src, int64_t i) {
     else return src[i];
 }
 
+// One output pixel of the transform (normalise, then bilinear resize with align_corners=False; ATen
+// area_pixel_compute_source_index) from image plane base xb [3][H][W]: the three channels and a zero
+// fourth.  Shared by the transform kernel and the SSD stem that folds the transform in, so both
+// produce the same bits.
+template <typename T>
+__device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int W, float sh, float sw,
+                                           const float* mean, const float* stdv, int oy, int ox) {
+    float ry = sh * ((float)oy + 0.5f) - 0.5f;
+    float rx = sw * ((float)ox + 0.5f) - 0.5f;
+    ry = ry < 0.f ? 0.f : ry;
+    rx = rx < 0.f ? 0.f : rx;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + ((y0 < H - 1) ? 1 : 0);
+    const int x1 = x0 + ((x0 < W - 1) ? 1 : 0);
+    const float ly = ry - (float)y0, lx = rx - (float)x0;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const T* src = xb + (int64_t)c * H * W;
+        const float a00 = (pre_load(src, (int64_t)y0 * W + x0) - mean[c]) / stdv[c];
+        const float a01 = (pre_load(src, (int64_t)y0 * W + x1) - mean[c]) / stdv[c];
+        const float a10 = (pre_load(src, (int64_t)y1 * W + x0) - mean[c]) / stdv[c];
+        const float a11 = (pre_load(src, (int64_t)y1 * W + x1) - mean[c]) / stdv[c];
+        v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
+    }
+    return f32x4{v[0], v[1], v[2], 0.f};
+}
+
 template <typename T>
 __global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -38,29 +67,7 @@ __global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int oy = (int)((idx / p.Wp) % p.Hp);
     const int b = (int)(idx / ((int64_t)p.Wp * p.Hp));
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
-    if (oy < p.Ho && ox < p.Wo) {
-        // ATen area_pixel_compute_source_index (align_corners=False, linear)
-        float ry = p.sh * ((float)oy + 0.5f) - 0.5f;
-        float rx = p.sw * ((float)ox + 0.5f) - 0.5f;
-        ry = ry < 0.f ? 0.f : ry;
-        rx = rx < 0.f ? 0.f : rx;
-        const int y0 = (int)ry, x0 = (int)rx;
-        const int y1 = y0 + ((y0 < p.H - 1) ? 1 : 0);
-        const int x1 = x0 + ((x0 < p.W - 1) ? 1 : 0);
-        const float ly = ry - (float)y0, lx = rx - (float)x0;
-        const float hy = 1.f - ly, hx = 1.f - lx;
-        float v[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const T* src = x + ((int64_t)b * 3 + c) * p.H * p.W;
-            const float a00 = (pre_load(src, (int64_t)y0 * p.W + x0) - p.mean[c]) / p.stdv[c];
-            const float a01 = (pre_load(src, (int64_t)y0 * p.W + x1) - p.mean[c]) / p.stdv[c];
-            const float a10 = (pre_load(src, (int64_t)y1 * p.W + x0) - p.mean[c]) / p.stdv[c];
-            const float a11 = (pre_load(src, (int64_t)y1 * p.W + x1) - p.mean[c]) / p.stdv[c];
-            v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
-        }
-        out = f32x4{v[0], v[1], v[2], 0.f};
-    }
+    if (oy < p.Ho && ox < p.Wo) out = pre_pixel(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, p.mean, p.stdv, oy, ox);
     *reinterpret_cast<f32x4*>(p.y + idx * 4) = out;
 }
 
@@ -312,6 +319,10 @@ constexpr int STEM_T = 16, STEM_SH = STEM_T + 2, STEM_XH = 2 * STEM_SH + 1, STEM
 // LDS weight image: w0 [16][36] (taps (kh, kw, ci)), b0 [16], wd [9][16], bd [16], w1 [16][16], b1 [16]
 constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 = 752, STEM_B1 = 1008, STEM_NW = 1024;
 
+// T = float: the transform's NHWC4 output (p.x); T = float / uint8_t with FUSED: the source image
+// (p.src / p.src8, [B][3][H0][W0]) and the transform computed per input pixel of the tile (pre_pixel,
+// the same bits as the transform kernel): no transform launch and no NHWC4 round trip through HBM.
+template <typename T, bool FUSED>
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
@@ -320,7 +331,7 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
     const int oh0 = (blockIdx.x / tiles_w) * STEM_T, ow0 = (blockIdx.x % tiles_w) * STEM_T;
     const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
     const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
-    const float* xb = p.x + (int64_t)b * p.H * p.W * 4;
+    const float* xb = FUSED ? nullptr : p.x + (int64_t)b * p.H * p.W * 4;
     {  // all of a thread's input pixels and weights in flight at once (one memory round trip)
         float wv[STEM_NW / 256];
 #pragma unroll
@@ -341,9 +352,15 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             const int v = tid + 256 * r;
             const int ih = xh0 + v / STEM_XH, iw = xw0 + v % STEM_XH;
             const bool in = v < STEM_XH * STEM_XH && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            const float* src = xb + (in ? ((int64_t)ih * p.W + iw) * 4 : 0);  // clamped: loads stay unconditional
-            xv[r] = *reinterpret_cast<const f32x4*>(src);
-            if (!in) xv[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (FUSED) {
+                const T* img = (const T*)(sizeof(T) == 1 ? (const void*)p.src8 : (const void*)p.src) +
+                               (int64_t)b * 3 * p.H0 * p.W0;
+                xv[r] = in ? pre_pixel(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, ih, iw) : f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+                const float* src = xb + (in ? ((int64_t)ih * p.W + iw) * 4 : 0);  // clamped: loads stay unconditional
+                xv[r] = *reinterpret_cast<const f32x4*>(src);
+                if (!in) xv[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -411,13 +428,26 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
         *reinterpret_cast<f32x4*>(yp + 4 * q) = f32x4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
 }
 
-int ssd_stem_launch(const StemParams& p, hipStream_t s) {
-    EDGEDET_REQUIRE(p.x && p.w0 && p.b0 && p.wd && p.bd && p.w1 && p.b1 && p.y, "ssd_stem: null pointer");
+int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
+    StemParams p = p0;
+    const bool fused = p.src || p.src8;
+    EDGEDET_REQUIRE((p.x || fused) && p.w0 && p.b0 && p.wd && p.bd && p.w1 && p.b1 && p.y, "ssd_stem: null pointer");
+    EDGEDET_REQUIRE(!(p.src && p.src8), "ssd_stem: one source image (float or uint8)");
+    if (fused) {
+        EDGEDET_REQUIRE(p.H0 >= 1 && p.W0 >= 1, "ssd_stem: source image size");
+        p.sh = (float)p.H0 / (float)p.H;  // as the transform kernel's input / output scales
+        p.sw = (float)p.W0 / (float)p.W;
+    }
     EDGEDET_REQUIRE(p.Ho == (p.H - 1) / 2 + 1 && p.Wo == (p.W - 1) / 2 + 1, "ssd_stem: 3x3 stride 2 pad 1 shape");
     EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
     const int tiles_w = cdiv(p.Wo, STEM_T);
-    hipLaunchKernelGGL(ssd_stem_kernel, dim3((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B), dim3(256), 0, s,
-                       p, tiles_w);
+    const dim3 grid((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B);
+    if (p.src8)
+        hipLaunchKernelGGL((ssd_stem_kernel<uint8_t, true>), grid, dim3(256), 0, s, p, tiles_w);
+    else if (p.src)
+        hipLaunchKernelGGL((ssd_stem_kernel<float, true>), grid, dim3(256), 0, s, p, tiles_w);
+    else
+        hipLaunchKernelGGL((ssd_stem_kernel<float, false>), grid, dim3(256), 0, s, p, tiles_w);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

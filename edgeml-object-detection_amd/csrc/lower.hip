@@ -632,8 +632,12 @@ class SSDLite {
         const int NC = cfg_.num_classes;
         const std::string sfx = nch > 1 ? "#" + std::to_string(c) : "";
         auto view = [&](int b) { return nch > 1 ? P.view(b, img0) : P.ref(b); };
-        const int x = P.buf({B, S, S, 4}, 4, "pre" + sfx);
-        {
+        // the transform (normalise 0.5 / 0.5, resize to S x S): folded into the fused stem's input loads
+        // (EDGEDET_SSD_STEM_FUSE=1, the default), else its own record into an NHWC4 buffer
+        const bool stem_fuse = env_int("EDGEDET_SSD_STEM_FUSE", 1) == 1 && !pack_only;
+        Cur cur;
+        if (!stem_fuse) {
+            const int x = P.buf({B, S, S, 4}, 4, "pre" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_PREPROCESS;
             o.name = "transform";
@@ -643,8 +647,8 @@ class SSDLite {
             o.p[1] = P.ref(x);
             for (int j = 0; j < 6; ++j) o.f[j] = 0.5f;
             P.add(o);
+            cur = Cur{P.ref(x), {B, S, S, 4}};
         }
-        Cur cur{P.ref(x), {B, S, S, 4}};
 
         auto conv = [&](const Cur& in, const std::string& prefix, int64_t cout, int k, int stride, int act,
                         Ref res = Ref(), Ref in_scale = Ref(), int64_t cin_pad = 0) {
@@ -760,8 +764,7 @@ class SSDLite {
         };
 
         int first = 0;
-        const bool stem_fuse = env_int("EDGEDET_SSD_STEM_FUSE", 1) == 1;
-        if (stem_fuse && !pack_only) {
+        if (stem_fuse) {
             ConvW w0 = cbn("backbone.features.0.0", 16, 3, 3, false, 4);
             Prefixes pf = block_prefixes(blocks_[0], "backbone.features.0.1.block");
             ConvW wd = cbn(pf.pd, 16, 16, 3, true);
@@ -771,10 +774,11 @@ class SSDLite {
             const int y = P.buf(ys, 4, "backbone.features.0.1" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SSD_STEM;
-            o.name = "backbone.features.0.0+0.1";
-            const int64_t iv[7] = {B, S, S, Ho, Wo, w0.Kpad, w1.Kpad};
-            for (int j = 0; j < 7; ++j) o.i[j] = iv[j];
-            o.p[0] = P.ref(x);
+            o.name = "transform+backbone.features.0.0+0.1";
+            const int64_t iv[9] = {B, S, S, Ho, Wo, w0.Kpad, w1.Kpad, H, W};
+            for (int j = 0; j < 9; ++j) o.i[j] = iv[j];
+            o.p[u8 ? 9 : 8] = view(inp);  // the source image; the transform runs in the stem's loads
+            for (int j = 0; j < 6; ++j) o.f[j] = 0.5f;
             o.p[1] = Plan::wref(w0.w);
             o.p[2] = Plan::wref(w0.b);
             o.p[3] = Plan::wref(wd.w);

@@ -310,7 +310,7 @@ class SSDLite320(_Detector):
         """Named buffers of the SSDLite plan the parity tests read (csrc/lower.hip SSDLite)."""
         P.cls_logits, P.bbox_regression = P.buffer("cls_logits"), P.buffer("bbox_regression")
         P.scores_t, P.boxes = P.buffer("scores_t"), P.buffer("boxes")
-        P.chains = max(1, sum(1 for n in P.buffers if n.startswith("pre#")))
+        P.chains = max(1, sum(1 for n in P.buffers if n.startswith("backbone.features.0.13#")))
 
 
 # ====================================================================================== FRCNN

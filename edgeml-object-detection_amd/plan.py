@@ -407,8 +407,13 @@ class NativePlan:
         self.input = self.buffer("images")
         self.out_box, self.out_score = self.buffer("out.boxes"), self.buffer("out.scores")
         self.out_label, self.out_count = self.buffer("out.labels"), self.buffer("out.count")
-        pre = next(op for op in self.ops if op.kind == ops.PREPROCESS)
-        self.resized = tuple(int(pre.i[j]) for j in (3, 4, 5, 6))  # (Ho, Wo, Hp, Wp) of the transform
+        # (Ho, Wo, Hp, Wp) of the transform: its own record, or the SSD stem that folds it in
+        pre = next((op for op in self.ops if op.kind == ops.PREPROCESS), None)
+        if pre is not None:
+            self.resized = tuple(int(pre.i[j]) for j in (3, 4, 5, 6))
+        else:
+            stem = next(op for op in self.ops if op.kind == ops.SSD_STEM)
+            self.resized = (int(stem.i[1]), int(stem.i[2]), int(stem.i[1]), int(stem.i[2]))
         self.graph = None
         model.attach(self)
         if self.device.type == "cuda":

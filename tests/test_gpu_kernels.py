@@ -168,6 +168,49 @@ def test_ssd_stem_matches_torch(B, H, W):
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("H0,W0,u8", [(640, 640, True), (480, 640, True), (427, 640, False), (37, 29, True)])
+def test_ssd_stem_folded_transform_bit_identical(H0, W0, u8):
+    """The SSD stem with the transform folded into its input loads (SSD_STEM record with a source image,
+    the plans' default) equals the transform record followed by the stem on its NHWC4 output, bit for
+    bit, for uint8 and float sources and resize ratios above and below 1."""
+    import ctypes
+    from edgeml_amd import ops
+    from edgeml_amd.plan import pack_conv_weight, pack_dw_weight
+    B, S = 3, 320
+    g = torch.Generator().manual_seed(H0 + W0)
+    img8 = torch.randint(0, 256, (B, 3, H0, W0), generator=g, dtype=torch.uint8)
+    src = (img8 if u8 else img8.float() / 255).to(DEV)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    w0p, _, ld0, _ = pack_conv_weight((torch.randn(16, 3, 3, 3, generator=g) / 5).numpy(), 4)
+    w1p, _, ld1, _ = pack_conv_weight((torch.randn(16, 16, 1, 1, generator=g) / 4).numpy())
+    wts = [dev(w0p), torch.randn(16, generator=g).to(DEV) * 0.1, dev(pack_dw_weight((torch.randn(16, 1, 3, 3, generator=g) / 3).numpy())),
+           torch.randn(16, generator=g).to(DEV) * 0.1, dev(w1p), torch.randn(16, generator=g).to(DEV) * 0.1]
+    x4 = torch.full((B, S, S, 4), float("nan"), device=DEV)
+    Ho = (S - 1) // 2 + 1
+    outs = [torch.full((B, Ho, Ho, 16), float("nan"), device=DEV) for _ in range(2)]
+    rec = np.zeros(3, dtype=ops.OP_DTYPE)
+    rec[0]["kind"] = ops.PREPROCESS
+    rec[0]["i"][:7] = [B, H0, W0, S, S, S, S]
+    rec[0]["p"][2 if u8 else 0] = src.data_ptr()
+    rec[0]["p"][1] = x4.data_ptr()
+    rec[0]["f"][:6] = 0.5
+    for k, fused in ((1, False), (2, True)):
+        rec[k]["kind"] = ops.SSD_STEM
+        rec[k]["i"][:9] = [B, S, S, Ho, Ho, ld0, ld1, H0 if fused else 0, W0 if fused else 0]
+        if fused:
+            rec[k]["p"][9 if u8 else 8] = src.data_ptr()
+            rec[k]["f"][:6] = 0.5
+        else:
+            rec[k]["p"][0] = x4.data_ptr()
+        for j, t in enumerate(wts):
+            rec[k]["p"][1 + j] = t.data_ptr()
+        rec[k]["p"][7] = outs[k - 1].data_ptr()
+    ops.check(ops.lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 3, ops.stream_handle()))
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("B,C,S,parts", [(1, 72, 24, 16), (32, 960, 240, 1), (7, 120, 32, 5), (64, 672, 168, 2),
                                           (33, 480, 120, 16)])
 def test_se_excitation_matches_torch(B, C, S, parts):

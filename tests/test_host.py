@@ -142,7 +142,10 @@ def test_ssd_plan_lowering():
     m = models.ssdlite320_mobilenet_v3_large()
     P = m.build_plan(4, 640, 480)
     kinds = [op.kind for op in P.ops]
-    assert kinds[0] == ops.PREPROCESS and kinds[-1] == ops.SSD_POSTPROCESS
+    # the transform is folded into the fused stem (its own record only with EDGEDET_SSD_STEM_FUSE=0)
+    assert ops.PREPROCESS not in kinds and ops.SSD_STEM in kinds and kinds[-1] == ops.SSD_POSTPROCESS
+    stem = P.ops[kinds.index(ops.SSD_STEM)]
+    assert [stem.i[k] for k in (1, 2, 7, 8)] == [320, 320, 640, 480] and P.resized == (320, 320, 320, 320)
     assert kinds.count(ops.FORK) == kinds.count(ops.JOIN) == 1
     pp = P.ops[-1]
     assert [pp.i[k] for k in range(5)] == [4, 3234, 91, 300, 300]
@@ -304,7 +307,7 @@ def test_ssd_chain_split_covers_the_batch(monkeypatch):
         monkeypatch.setenv("EDGEDET_SSD_CHAINS", str(n))
         native.release("ssd", B, 320, 320)
         P = m.build_plan(B, 320, 320)
-        parts = [P.buffer(f"pre#{c}").shape[0] for c in range(P.chains)] if P.chains > 1 else [B]
+        parts = [P.buffer(f"backbone.features.0.13#{c}").shape[0] for c in range(P.chains)] if P.chains > 1 else [B]
         assert P.chains == want and sum(parts) == B and max(parts) - min(parts) <= 1
         assert parts == sorted(parts, reverse=True)
         native.release("ssd", B, 320, 320)
