@@ -507,6 +507,14 @@ struct MbwGeom {
     static size_t smem(int nw) { return 4 * ((size_t)NPXP * (XS + 1) + (size_t)nw * (EW + P * ES)); }
 };
 
+// A workgroup barrier for LDS traffic only: __syncthreads' workgroup fence also waits for every
+// outstanding global load and store (vmcnt(0)), which would land the next tile's halo prefetch and the
+// previous tile's output stores on each barrier; the waves of this kernel exchange data through LDS
+// only.
+__device__ __forceinline__ void mbw_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ void mbw_wave_sync() {  // this wave's LDS writes visible to its own lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -576,6 +584,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
         hdst[u] = t < NPXP * Q4 ? px * XS + 4 * c4 : -1;
     }
     const int mr = tid < NPXP ? tid / IWh : 0, mc = tid % IWh;  // this thread's mask pixel (tid < NPXP)
+    uint32_t hok = 0;
     auto load_halo = [&](int tile) {
         const int b = tile / tiles_img, r = tile - b * tiles_img, th = r / tiles_w, tw = r - th * tiles_w;
         const int ih0 = th * TH * S - p.pad, iw0 = tw * TW * S - p.pad;
@@ -583,13 +592,14 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
 #pragma unroll
         for (int u = 0; u < HR; ++u) {
             const int ih = ih0 + hr[u], iw = iw0 + hc[u];
-            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-            if (diag & 2) {
-                hv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-                continue;
-            }
-            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + (ok ? (ih * p.W + iw) * Cin + hoff[u] : 0));
-            hv[u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && !(diag & 2);
+            // one load path: the offset is zeroed (not selected) outside the image, and the value is
+            // kept raw with an in-image bit; the select happens where it is stored, a tile later, so
+            // nothing waits on these loads until then (a select or a conditional address here made the
+            // compiler branch around the load and wait for every prefetch right after issuing it)
+            const int off = ((ih * p.W + iw) * Cin + hoff[u]) * (int)ok;
+            hv[u] = *reinterpret_cast<const f32x4*>(xb + off);
+            hok = (hok & ~(1u << u)) | ((uint32_t)ok << u);
         }
     };
     int tile = blockIdx.x;
@@ -597,15 +607,16 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
     for (; tile < ntiles; tile += gridDim.x) {
         const int b = tile / tiles_img, r = tile - b * tiles_img, th = r / tiles_w, tw = r - th * tiles_w;
         const int oh0 = th * TH, ow0 = tw * TW, ih0 = oh0 * S - p.pad, iw0 = ow0 * S - p.pad;
-        __syncthreads();  // the previous tile's reads of xs and of the partials are done
+        mbw_lds_barrier();  // the previous tile's reads of xs and of the partials are done
 #pragma unroll
         for (int u = 0; u < HR; ++u) {
             if (hdst[u] >= 0) {
+                const f32x4 v = (hok >> u) & 1 ? hv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
                 float* d = xs + hdst[u];
-                d[0] = hv[u].x;
-                d[1] = hv[u].y;
-                d[2] = hv[u].z;
-                d[3] = hv[u].w;
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
             }
         }
         if (tid < NPXP) {  // NPXP <= 4 waves of threads (the launcher's minimum)
@@ -613,7 +624,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
             xm[tid] = tid < NPX && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W ? 1.f : 0.f;
         }
         if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);
-        __syncthreads();
+        mbw_lds_barrier();
         // expand: the wave's 16 channels over every halo pixel, two accumulation chains at a time
         // (x 0 outside the image: the depthwise conv zero-pads the expanded tensor)
         auto expand_store = [&](const f32x4& a, int t) {
@@ -684,7 +695,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
             for (int n = 0; n < 2; ++n)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) es[(16 * t + 4 * q + i) * PS + 16 * n + l16] = acc[t][n][i];
-        __syncthreads();
+        mbw_lds_barrier();
         // partials added in wave order, bias, residual (S == 1: the input pixel at the tap centre), store
         const float* part = mb_smem + NPXP * XS;
         for (int e = tid; e < P * 32; e += nt) {
