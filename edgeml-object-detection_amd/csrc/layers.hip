@@ -522,7 +522,7 @@ __device__ __forceinline__ void mbw_wave_sync() {  // this wave's LDS writes vis
 }
 
 template <int K, int S, int ACT, int CINP, int TH, int TW>
-__global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, int tiles_w, int tiles_img, int ntiles, int diag) {
+__global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, int tiles_w, int tiles_img, int ntiles) {
     using G = MbwGeom<K, S, CINP, TH, TW>;
     constexpr int IWh = G::IWh, NPX = G::NPX, NPXP = G::NPXP, P = G::P;
     constexpr int XS = G::XS, ES = G::ES, PS = G::PS, EW = G::EW;
@@ -592,7 +592,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
 #pragma unroll
         for (int u = 0; u < HR; ++u) {
             const int ih = ih0 + hr[u], iw = iw0 + hc[u];
-            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && !(diag & 2);
+            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             // one load path: the offset is zeroed (not selected) outside the image, and the value is
             // kept raw with an in-image bit; the select happens where it is stored, a tile later, so
             // nothing waits on these loads until then (a select or a conditional address here made the
@@ -635,7 +635,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
             }
         };
 #pragma unroll 1
-        for (int t = 0; t < (diag & 8 ? 0 : NT); t += 2) {
+        for (int t = 0; t < NT; t += 2) {
             f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
             const float* r0 = xs + (16 * t + l16) * XS + q;
 #pragma unroll
@@ -649,7 +649,7 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
         mbw_wave_sync();
         // depthwise: lane = (channel l16, output rows q, q + 4, ...), a K x K window slid along the row
 #pragma unroll 1
-        for (int oy = q; oy < (diag & 4 ? 0 : TH); oy += 4) {
+        for (int oy = q; oy < TH; oy += 4) {
             float win[K][K];
 #pragma unroll
             for (int kh = 0; kh < K; ++kh)
@@ -706,14 +706,9 @@ __global__ void __launch_bounds__(64 * MBW_MAXW, 4) mbconv_kernel(MbParams p, in
             for (int w = 1; w < nw; ++w) v += part[w * EW + px * PS + co];
             v += b2v;
             if (p.residual) v += xs[((ly + p.pad) * IWh + lx + p.pad) * XS + co];
-            if (!(diag & 1)) p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
+            p.y[(((int64_t)b * p.Ho + oh) * p.Wo + ow) * Cout + co] = v;
         }
     }
-}
-
-static int env_flag_int(const char* k) {
-    const char* e = std::getenv(k);
-    return e ? std::atoi(e) : 0;
 }
 
 // Opt an instantiation into its dynamic LDS once per process (not a stream operation: legal while a
@@ -745,10 +740,7 @@ static int mbconv_launch_t(const MbParams& p, hipStream_t s) {
     // halo loaded under the previous tile's compute
     const int per_cu = std::max(1, (int)((160 * 1024) / lds));
     const int grid = std::min(ntiles, 256 * per_cu);
-    // EDGEDET_MB_DIAG (diagnostic only, wrong results): 1 no output stores, 2 no halo loads, 4 no
-    // depthwise, 8 no expansion
-    static const int diag = env_flag_int("EDGEDET_MB_DIAG");
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * nw), lds, s, p, tiles_w, tiles_img, ntiles, diag);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * nw), lds, s, p, tiles_w, tiles_img, ntiles);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
