@@ -1266,9 +1266,12 @@ class FasterRCNN : public ResNetFPN {
         const int Aa = 3;
         std::vector<std::pair<Ref, Ref>> heads;
         std::vector<std::pair<int, int>> grids;
-        P.fork(3);
+        // the five levels in order on the caller stream (EDGEDET_RPN_LANES=1: on four stream lanes, 0.75 %
+        // slower at two plans in flight, tools/gpu_r3ab.sh: eight streams over four hardware queues)
+        const bool rpn_lanes = env_int("EDGEDET_RPN_LANES", 0) == 1;
+        if (rpn_lanes) P.fork(3);
         for (size_t lvl = 0; lvl < outs.size(); ++lvl) {
-            P.lane((int)(lvl % 4));
+            if (rpn_lanes) P.lane((int)(lvl % 4));
             const std::string at = "@" + std::to_string(lvl);
             Cur t = conv_b(P, outs[lvl], "rpn.head.conv.0.0", 256, 3, 1, A_RE, "rpn.head.conv.0" + at);
             t = conv_b(P, t, "rpn.head.conv.1.0", 256, 3, 1, A_RE, "rpn.head.conv.1" + at);
@@ -1277,7 +1280,7 @@ class FasterRCNN : public ResNetFPN {
             heads.push_back({o.x, d.x});
             grids.push_back({(int)outs[lvl].s[1], (int)outs[lvl].s[2]});
         }
-        P.join();
+        if (rpn_lanes) P.join();
         std::vector<int> anchor_bufs;
         const int sizes[5] = {32, 64, 128, 256, 512};
         for (size_t l = 0; l < grids.size(); ++l) {
