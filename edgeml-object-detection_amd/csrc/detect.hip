@@ -1668,7 +1668,9 @@ int merge_topk_launch(const MergeParams& P, int B, hipStream_t s) {
                     "merge_topk: null pointer");
     EDGEDET_REQUIRE(P.N <= 1024 && P.N > 0 && P.S > 0 && P.kmax > 0, "merge_topk: bad sizes");
     EDGEDET_REQUIRE(P.S < 1024, "merge_topk: at most 1023 segments");
-    constexpr int KC = 1024, NT = 512, PER = 64;
+    // PER = 16 register slots per thread (8,192 candidates on the register path, the radix path above
+    // that): at 64 the kernel took 202 VGPRs and 272 B of scratch per lane
+    constexpr int KC = 1024, NT = 512, PER = 16;
     auto k = merge_topk_kernel<NT, KC, PER>;
     if (set_lds(k, seg_smem<KC>())) return -2;
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), seg_smem<KC>(), s, P);
