@@ -72,32 +72,59 @@ def step(plan, stream, d2h):
             host.copy_(dev, non_blocking=True)
 
 
+TIMING = {}  # how the last timed_steps call measured (reported on the JSON line)
+
+
 def timed_steps(plan, stream, steps, warmup, dist, extra=()):
-    """Time `steps` whole-batch passes (forward graph + D2H of the detections). With `extra` =
-    [(plan, stream), ...] the passes rotate over independent plan instances (own arena, own graph,
-    own pinned output buffers) on their own streams, so batch k+1's first convolutions overlap batch
-    k's low-occupancy NMS tail; every pass is still a complete forward of its own batch, and each
-    instance's passes stay ordered on its stream."""
+    """Seconds for `steps` whole-batch passes (forward graph + D2H of the detections) in steady state.
+
+    With `extra` = [(plan, stream), ...] the passes rotate over independent plan instances (own arena,
+    own graph, own pinned output buffers) on their own streams, so batch k+1's first convolutions
+    overlap batch k's low-occupancy NMS tail; every pass is still a complete forward of its own batch,
+    and each instance's passes stay ordered on its stream.
+
+    Steady state (round 4): a completion event is recorded on the instance's stream after each pass's
+    D2H.  The pipeline is NOT drained between the warmup and the timed passes, so the timed region
+    starts full, as in a long run: the time is (completion of the last timed pass) - (completion of
+    the last warmup pass), K completions at the steady rate, with no fill or drain latency in the
+    denominator.  Every instance was primed when it was captured (graph uploaded and replayed,
+    plan.capture), and the warmup covers each instance at least once.  The ranks start together
+    (barrier + device sync before the warmup) and end together (device sync + barrier after the
+    last pass); the max over ranks is taken.  The host wall clock of the same K passes (timed from
+    the first timed issue to the final sync, so it includes the drain) is kept in TIMING."""
     lanes = [(p, s, d2h_buffers(p)) for p, s in [(plan, stream)] + list(extra)]
-    for i in range(warmup):
-        step(*lanes[i % len(lanes)])
-    for _, s, _ in lanes:
-        s.synchronize()
+    n = len(lanes)
+    warm = max(warmup, n)
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    for i in range(warm):
+        step(*lanes[i % n])
+    mark = torch.cuda.Event(enable_timing=True)
+    mark.record(lanes[(warm - 1) % n][1])
+    done = []
     t0 = time.perf_counter()
     for i in range(steps):
-        step(*lanes[i % len(lanes)])
+        p, s, d2h = lanes[(warm + i) % n]
+        step(p, s, d2h)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(s)
+        done.append(e)
     for _, s, _ in lanes:
         s.synchronize()
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    wall = time.perf_counter() - t0
+    el = max(mark.elapsed_time(e) for e in done) / 1e3
     if dist:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([el, wall], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el, wall = (float(v) for v in t.tolist())
+    TIMING.clear()
+    TIMING.update({"method": "steady state: K pass completions (HIP events after each pass's D2H) from the "
+                             "last warmup completion; pipeline kept full across the start",
+                   "device_s": round(el, 6), "wall_s_incl_drain": round(wall, 6), "warmup_passes": warm,
+                   "instances": n})
     return el
 
 
@@ -204,10 +231,6 @@ def op_work(op):
         return "conv", flops, byts
     if k == O.DWCONV:
         B, H, W, C, Ho, Wo, K = (i[j] for j in range(7))
-        if op.p.get(5) is not None:  # fused MBConv front: 1x1 expansion of the Cin-wide input + depthwise
-            cin = i[11]
-            return ("mbconv", 2.0 * B * (H * W * C * cin + Ho * Wo * C * K * K),
-                    4.0 * (B * H * W * cin + B * Ho * Wo * C + C * (cin + K * K)))
         return "dwconv", 2.0 * B * Ho * Wo * C * K * K, 4.0 * (B * H * W * C + B * Ho * Wo * C + C * K * K)
     if k == O.SSD_STEM:  # stem conv 3x3 s2 (4 -> 16) + depthwise 3x3 + projection 16 -> 16 + residual
         B, H, W, Ho, Wo = (i[j] for j in range(5))
@@ -253,14 +276,6 @@ def op_work(op):
         return "retina_select", 0.0, 4.0 * i[0] * n * (i[3] + 4)
     if k == O.RETINA_CLASS_NMS:
         return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
-    if k == O.SSD_HEADS:  # per map: feature map in, depthwise + 1x1 weights, head outputs
-        B, nm, cols = i[0], i[1], i[4]
-        fl, by = 0.0, 0.0
-        for m in range(nm):
-            H, W, C = i[5 + 8 * m], i[6 + 8 * m], i[7 + 8 * m]
-            fl += 2.0 * B * H * W * C * (9 + 6 * cols)
-            by += 4.0 * (B * H * W * C + 10 * C + 6 * cols * (C + 1) + B * H * W * 6 * cols)
-        return "ssd_heads", fl, by
     if k == O.MBCONV:  # expand 1x1 + depthwise KxK + project 1x1 (+ residual): block input in, output out
         B, H, W, Cin, Cexp, Cout, Ho, Wo, K = (i[j] for j in range(9))
         fl = 2.0 * B * (H * W * Cin * Cexp + Ho * Wo * Cexp * (K * K + Cout))
@@ -382,13 +397,44 @@ def _cpu_model():
     return None
 
 
+G5 = os.path.join(ROOT, "tests", "golden", "g5_orie_f64.npz")  # float64 ground truth (make_orie_f64.py)
+
+
+def _f64_truth(n):
+    """The float64 detector files of G5 for the leg's n images ({"weak"/"strong": [rows]}) and the
+    per-image input checksums they were made from; None if absent or too short."""
+    try:
+        z = np.load(G5)
+    except OSError:
+        return None
+    if len(z["image_sums"]) < n:
+        return None
+    out = {"sums": z["image_sums"][:n]}
+    for tag in ("weak", "strong"):
+        cnt = z[tag + "_f64_count"]
+        off = np.concatenate([[0], np.cumsum(cnt)])
+        out[tag] = [z[tag + "_f64_rows"][off[i]:off[i + 1]] for i in range(n)]
+    return out
+
+
 def orie_vs_ref(n=48, E=None):
     """ORIE of the engine's files vs ORIE of the CPU oracle's files on n synthetic 640x640 images
-    (SSDLite weak, FRCNN strong; pseudo ground truth = the oracle strong detector's confident boxes),
-    E = n - 1 so every image is in every ensemble, as in config 4 (E = 1000 over 5,000): the engine
-    side goes through the product consumer (GPU reward), the reference side through the oracle
-    consumer (oracle/orie.py, pinned to the reference's own G2 values).  The oracle's batch=1 CPU
-    forwards are timed on the way: they are the FRCNN cpu_baseline (same images, same loop)."""
+    (SSDLite weak, FRCNN strong), E = n - 1 so every image is in every ensemble, as in config 4
+    (E = 1000 over 5,000).  Three sets of detect.py files for the same images:
+      engine    the HIP engine (batch=1 per image), through the product consumer (GPU reward) for
+                the metric's ORIE max-abs-diff;
+      oracle    the CPU oracle in float32 (its batch=1 forwards are timed on the way: they are the
+                FRCNN cpu_baseline), through the oracle consumer (pinned to the reference's G2);
+      f64       the same oracle with every conv / linear / BN / activation in float64 and the head
+                outputs rounded to float32 before the reference's float32 post-processing
+                (tests/golden/g5_orie_f64.npz, made by tests/golden/make_orie_f64.py from the same
+                seeded inputs; the input checksums are verified here): the exact-arithmetic detector
+                both float32 implementations approximate.
+    Pseudo ground truth for all three = the f64 strong detector's confident boxes (conf >= 0.3).
+    Reported: max |ORIE(engine) - ORIE(oracle)| (the metric); ORIE(engine) - ORIE(f64) beside
+    ORIE(oracle) - ORIE(f64), all three through the oracle consumer; and identity-paired file
+    differences (tools/rowpair.py: rows paired by class and IoU >= 0.99, paired |dconf| / |dbox|,
+    unpaired counts) for each pair of sets and detector."""
     import tempfile
     import warnings
     from edgeml_amd import fmt, models, reward, synthetic
@@ -396,19 +442,24 @@ def orie_vs_ref(n=48, E=None):
     from oracle.frcnn import FasterRCNNOracle
     from oracle.ssdlite import SSDLiteOracle
     from edgeml_amd.distributed import usable_cpus
+    from tools import rowpair
     warnings.filterwarnings("ignore")
     torch.set_num_threads(usable_cpus())
     E = n - 1 if E is None else E
     cpu_s = {"weak": 0.0, "strong": 0.0}
+    truth = _f64_truth(n)
     sd_w, sd_s = synthetic.synthetic_state_dict("ssd", 91, True), synthetic.synthetic_state_dict("faster_rcnn", 91)
     eng = {"weak": models.SSDLite320(sd_w, 91, True).to("cuda"), "strong": models.FasterRCNNFPNv2(sd_s, 91).to("cuda")}
     ref = {"weak": SSDLiteOracle(sd_w, 91, True), "strong": FasterRCNNOracle(sd_s, 91)}
+    sets = ("eng", "ref", "f64")
     with tempfile.TemporaryDirectory() as td:
         d = lambda *p: os.path.join(td, *p)  # noqa: E731
-        for sub in ("eng_weak", "eng_strong", "ref_weak", "ref_strong", "labels"):
+        for sub in [s_ + "_" + t for s_ in sets for t in ("weak", "strong")] + ["labels"]:
             os.makedirs(d(sub))
         for i in range(n):
             img = synthetic.make_batch(1, 640, 640, seed=7000 + i)
+            if truth is not None and float(img.double().sum()) != float(truth["sums"][i]):
+                truth = None  # regenerated inputs differ from G5's: no f64 leg
             name = f"{i:012d}.png"
             for tag in ("weak", "strong"):
                 p = eng[tag](img.cuda())[0]
@@ -420,30 +471,45 @@ def orie_vs_ref(n=48, E=None):
                     cpu_s[tag] += time.perf_counter() - t0
                 rows = fmt.format_detections(q["boxes"].numpy(), q["scores"].numpy(), q["labels"].numpy(), 640, 640)
                 fmt.save_npy(d("ref_" + tag), name, rows)
-                if tag == "strong":
-                    with open(d("labels", name[:-4] + ".txt"), "w") as f:
-                        for r in rows[rows[:, 5] >= 0.3]:
-                            f.write(" ".join([str(int(r[0]))] + [repr(float(v)) for v in r[1:5]]) + "\n")
-        # where the ORIE difference comes from: per detector, the images whose files differ
-        # in structure (row count or label sequence: a boundary flip or a reordering), and the largest
-        # value difference over the structurally equal files (fp32 summation order)
+        have_f64 = truth is not None
+        for i in range(n):
+            name = f"{i:012d}.png"
+            if have_f64:
+                for tag in ("weak", "strong"):
+                    fmt.save_npy(d("f64_" + tag), name, truth[tag][i])
+            src = truth["strong"][i] if have_f64 else np.load(d("ref_strong", name[:-4] + ".npy"))
+            with open(d("labels", name[:-4] + ".txt"), "w") as f:
+                for r in src[src[:, 5] >= 0.3]:
+                    f.write(" ".join([str(int(r[0]))] + [repr(float(v)) for v in r[1:5]]) + "\n")
+        names = [f"{i:012d}" for i in range(n)]
+        load = lambda side, tag: (lambda nm: np.load(d(side + "_" + tag, nm + ".npy")))  # noqa: E731
         files = {}
-        for tag in ("weak", "strong"):
-            structural, max_val = 0, 0.0
-            for i in range(n):
-                a, b = (np.load(d(side + "_" + tag, f"{i:012d}.npy")) for side in ("eng", "ref"))
-                if a.shape != b.shape or not np.array_equal(a[:, 0], b[:, 0]):
-                    structural += 1
-                elif len(a):
-                    max_val = max(max_val, float(np.abs(a - b).max()))
-            files[tag] = {"structural": structural, "max_value_diff": max_val}
+        for a_, b_ in (("eng", "ref"), ("eng", "f64"), ("ref", "f64")):
+            if "f64" in (a_, b_) and not have_f64:
+                continue
+            files[f"{a_}_vs_{b_}"] = {tag: rowpair.compare_dirs(names, load(a_, tag), load(b_, tag))
+                                      for tag in ("weak", "strong")}
         wd, sd, lab = reward.set_data(d("eng_weak"), d("eng_strong"), d("labels"))
-        got = reward.compute_orie_all(wd, sd, lab, E, seed=1000)
-        want = orie.orie_all(d("ref_weak"), d("ref_strong"), d("labels"), E, seed=1000)
-    d = np.abs(got - want)
-    out = {"max_abs_diff": float(d.max()), "images": n, "num_ensemble": E,
-           "images_differing": int(np.count_nonzero(d)), "nonzero_ref": int(np.count_nonzero(want)),
-           "files": files}
+        got = reward.compute_orie_all(wd, sd, lab, E, seed=1000)  # engine files, product (GPU) consumer
+        cons = {s_: orie.orie_all(d(s_ + "_weak"), d(s_ + "_strong"), d("labels"), E, seed=1000)
+                for s_ in sets if s_ != "f64" or have_f64}  # every set through the oracle consumer
+    want = cons["ref"]
+    dd = np.abs(got - want)
+    out = {"max_abs_diff": float(dd.max()), "images": n, "num_ensemble": E,
+           "images_differing": int(np.count_nonzero(dd)), "nonzero_ref": int(np.count_nonzero(want)),
+           "consumer_check_max_abs": float(np.abs(got - cons["eng"]).max()),
+           "files_paired": files}
+    if have_f64:
+        t = cons["f64"]
+        de, do = np.abs(cons["eng"] - t), np.abs(cons["ref"] - t)
+        out["vs_f64"] = {"engine_max_abs": float(de.max()), "oracle_f32_max_abs": float(do.max()),
+                         "engine_images_differing": int(np.count_nonzero(de)),
+                         "oracle_f32_images_differing": int(np.count_nonzero(do)),
+                         "engine_mean_abs": float(de.mean()), "oracle_f32_mean_abs": float(do.mean()),
+                         "truth": "tests/golden/g5_orie_f64.npz (oracle forward in float64, heads rounded to "
+                                  "float32, float32 post-processing)"}
+    else:
+        out["vs_f64"] = None
     frcnn_cpu = {"value": round((n - 1) / cpu_s["strong"], 3), "unit": "images/s", "cores": torch.get_num_threads(),
                  "kind": "port", "host_cores": os.cpu_count(), "host_cpu": _cpu_model(),
                  "sample": f"{n - 1} synthetic 640x640 images, batch=1 ({cpu_s['strong']:.1f}s), frcnn CPU oracle "
@@ -495,6 +561,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dump-ops", default="", help="write the per-op device times of each model to this JSON")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host uint8 -> rows) rates")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="allow EDGEDET_DIAG_SKIP (diagnostic builds only); the line is marked and is not a result")
     ap.add_argument("--e2e-batches", type=int, default=40)
     ap.add_argument("--input", default="u8", choices=["u8", "f32"],
                     help="what the step's input batch in HBM holds: the decoded uint8 images (the detect CLI's "
@@ -502,6 +570,11 @@ def main():
                          "or the model contract's float images")
     args = ap.parse_args()
     u8 = args.input == "u8"
+    # EDGEDET_DIAG_SKIP (honoured only by a -DEDGEDET_DIAG build, libedgedet_diag.so) leaves op families
+    # out: wrong results, so a measurement under it is never a product number
+    if os.environ.get("EDGEDET_DIAG_SKIP") and not args.diagnostic:
+        sys.exit("bench.py: EDGEDET_DIAG_SKIP is set (a diagnostic that skips work, wrong results); "
+                 "refusing to measure without --diagnostic")
 
     dist, rank, world = dist_setup(args.gpus)
     from edgeml_amd import models, synthetic
@@ -518,7 +591,8 @@ def main():
         extra = inflight_instances(m, B, nin, 100 * rank, u8)
         el = timed_steps(plan, stream, args.steps, args.warmup, dist, extra)
         out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
-                      "inflight": nin, "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
+                      "inflight": nin, "dets_per_img": float(plan.out_count.tensor().float().mean().item()),
+                      "timing": dict(TIMING)}
         # SURVEY §8(d)'s binding roof for C2: 87.1 MB of algorithmic HBM traffic per image with the fp32
         # input image (4.92 MB); a uint8 input batch reads 1.23 MB of it instead
         bpi = SSD_BYTES_PER_IMG - (3 * 640 * 640 * 3 if u8 else 0)
@@ -565,12 +639,13 @@ def main():
         extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 50, u8)
         steps = max(20, args.steps // 10)  # FRCNN steps are ~20x SSD's: at least 20 (about half a second)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
+        timing = dict(TIMING)
         del extra
         R = float(plan.proposal_count.tensor().float().mean().item())
         gflop = 2 * (151.45e9 + 128.92e6 * R) / 1e9
         out["frcnn"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
                         "proposals_per_img": R, "dets_per_img": float(plan.out_count.tensor().float().mean().item()),
-                        "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2)}
+                        "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2), "timing": timing}
         if rank == 0 and not args.no_roofline:
             out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "frcnn")
             attach_traffic(out["frcnn"]["roofline"], "frcnn")
@@ -617,10 +692,12 @@ def main():
         line["retinanet"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in f.items()}
     if "roofline" in p:
         line["roofline"] = p["roofline"]
+    if os.environ.get("EDGEDET_DIAG_SKIP"):
+        line["diagnostic"] = "EDGEDET_DIAG_SKIP=%s: op families skipped, NOT a result" % os.environ["EDGEDET_DIAG_SKIP"]
     line["dets_per_img"] = p.get("dets_per_img")
     if "end_to_end" in p:
         line["end_to_end"] = p["end_to_end"]
-    for k in ("step_hbm", "alt_inflight"):
+    for k in ("step_hbm", "alt_inflight", "timing"):
         if k in p:
             line[k] = p[k]
     if not args.no_cpu:

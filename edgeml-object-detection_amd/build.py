@@ -58,17 +58,23 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in _deps())
 
 
-def build(force=False, verbose=False, jobs=8):
-    if not force and up_to_date():
+DIAG_LIB = os.path.join(HERE, "libedgedet_diag.so")
+
+
+def build(force=False, verbose=False, jobs=8, diag=False):
+    """diag=True: libedgedet_diag.so with -DEDGEDET_DIAG (the EDGEDET_DIAG_SKIP op-family skips of
+    csrc/exec.hip, wrong results; load it with EDGEDET_LIB, tools/gpu_skip.sh).  Never the product."""
+    lib = DIAG_LIB if diag else LIB
+    if not force and not diag and up_to_date():
         return LIB
     cc = hipcc()
-    objdir = os.path.join(HERE, "build")
+    objdir = os.path.join(HERE, "build_diag" if diag else "build")
     os.makedirs(objdir, exist_ok=True)
     write_tile_table(objdir)
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
-        cmd = [cc, *FLAGS, "-I", objdir, "-c", src, "-o", obj]
+        cmd = [cc, *FLAGS, *(["-DEDGEDET_DIAG"] if diag else []), "-I", objdir, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -78,13 +84,14 @@ def build(force=False, verbose=False, jobs=8):
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, sources()))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     r = subprocess.run([cc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(tmp, LIB)
-    build_native_host(cc)
-    return LIB
+    os.replace(tmp, lib)
+    if not diag:
+        build_native_host(cc)
+    return lib
 
 
 HOST_SRC = os.path.join(os.path.dirname(HERE), "tools", "native_host.cpp")
@@ -107,4 +114,4 @@ def build_native_host(cc=None):
 
 if __name__ == "__main__":
     import sys
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

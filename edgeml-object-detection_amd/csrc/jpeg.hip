@@ -661,9 +661,9 @@ extern "C" int64_t edgedet_jpeg_packet(const uint8_t* data, int64_t size, void* 
 // 256 B, then the packets, each 256-B aligned (placed in completion order; the offsets say where).
 // hw[2i..2i+1] = (H, W) of file i; *max_plane_bytes = the largest nblocks * 64 of the batch.  Returns the
 // bytes the batch image spans (the upload); when that exceeds `cap` nothing usable was written and the
-// caller retries with a buffer of the returned size.  0 = a file the device path does not handle (the
-// caller decodes the batch on the host; edgedet_last_error says which and why), < 0 = unreadable or
-// malformed file.  Replaces a Python thread pool calling edgedet_jpeg_packet per file, whose per-file
+// caller retries with a buffer of the returned size.  0 = a file the device path does not handle or
+// rejects as malformed (the caller decodes the batch on the host; edgedet_last_error says which and
+// why), < 0 = a file that cannot be opened or read.  Replaces a Python thread pool calling edgedet_jpeg_packet per file, whose per-file
 // Python work and pinned allocations kept the detect CLI at a quarter of the entropy decoders' rate.
 extern "C" int64_t edgedet_jpeg_batch_packets(const char* const* paths, int64_t n, void* out, int64_t cap,
                                               int32_t* hw, int64_t* max_plane_bytes, int32_t threads) {
@@ -703,7 +703,11 @@ extern "C" int64_t edgedet_jpeg_batch_packets(const char* const* paths, int64_t 
             Decoder dec;
             const int64_t m = dec.run(file.data(), file.size(), binfo, coef);
             if (m <= 0) {
-                fail(m == 0 ? 0 : (int)m, std::string("edgedet: jpeg: ") + paths[i] + ": " + dec.err);
+                // a file this decoder rejects — unsupported, not a JPEG at all (a PNG named .jpg), or
+                // entropy data it cannot parse (libjpeg only warns on those and still decodes) — makes
+                // the batch "unsupported": the caller decodes it on the host, as the reference's
+                // read_image would.  Only an unreadable file is an error.
+                fail(0, std::string("edgedet: jpeg: ") + paths[i] + ": " + (m == 0 ? "" : "rejected: ") + dec.err);
                 return;
             }
             hw[2 * i] = dec.H;

@@ -61,18 +61,6 @@ struct MbParams {
 };
 int mbconv_launch(const MbParams& p, hipStream_t s);
 
-// SSDLite head branches of the small feature maps (maps 1..5: 10x10 and below) in one launch: per map
-// depthwise 3x3 + folded BN + ReLU6, then the 1x1 conv with bias, stored into the concatenated head
-// output.  Weights are float offsets from w (the packed blob).
-struct SsdHeadsParams {
-    const float* w;
-    const float* feat[5];
-    float* out;  // [Btot][A][cols]
-    int B, nmaps, A, img0, cols;
-    int H[5], W[5], C[5], a0[5];
-    int64_t dw_w[5], dw_b[5], cw[5], cb[5];
-};
-int ssd_heads_launch(const SsdHeadsParams& p, hipStream_t s);
 
 struct PoolParams {
     const float* x;

@@ -779,149 +779,6 @@ int mbconv_launch(const MbParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(false, "mbconv: K in {3, 5}, stride in {1, 2}");
 }
 
-// ------------------------------------------------------------------------------ SSDLite small heads
-// SSDLiteHead on feature maps 1..5 (10x10 .. 1x1): per map and branch,
-// [dw3x3 + BN + ReLU6, 1x1 conv with bias], 10 layers x 2 ops that each launch a few thousand
-// threads for a few microseconds, as one launch per branch.  Block = (map, 64-wide output tile,
-// image): the map is processed in 32-channel chunks through LDS — the chunk of the feature map, its
-// depthwise output (taps in (kh, kw) order, out-of-map taps skipped, as the depthwise kernels), and the
-// chunk's 1x1 weights; each output accumulates over the channels in order (fp32 fma).  Every global load of a
-// chunk is issued at once into registers one chunk ahead (a strided load-then-store loop would wait
-// out one memory round trip per element).  Outputs go to the concatenated head tensor at (image, map
-// anchor offset + pixel * 6 * cols + n), as the strided conv epilogue stores them.
-// 1x1 register block: thread (nl = tid & 15, pg = tid >> 4) owns outputs n0 + nl + 16k (k < 4) at
-// pixels pg + 16q (q < 7), so one LDS read of a depthwise value feeds four FMAs.
-constexpr int HD_CC = 32, HD_NT = 64, HD_MAXP = 100, HD_NO = HD_NT / 16, HD_PQ = (HD_MAXP + 15) / 16;
-constexpr int HD_FQ = (HD_MAXP * HD_CC / 4 + 255) / 256;  // feature f32x4 per thread per chunk
-constexpr int HD_WQ = HD_NT * HD_CC / 256;                // 1x1 weights per thread per chunk
-constexpr int HD_DQ = (9 * HD_CC + HD_CC + 255) / 256;    // depthwise taps + bias per thread per chunk
-
-__global__ void __launch_bounds__(256) ssd_heads_kernel(SsdHeadsParams p) {
-    __shared__ float fs[HD_MAXP * (HD_CC + 1)];
-    __shared__ float ds[HD_MAXP * (HD_CC + 1)];
-    __shared__ float wc[HD_NT * (HD_CC + 1)];
-    __shared__ float wdw[10 * HD_CC];  // 9 taps, then the bias
-    const int nout = 6 * p.cols, ntiles = (nout + HD_NT - 1) / HD_NT;
-    const int m = blockIdx.x / ntiles, t = blockIdx.x - m * ntiles, b = blockIdx.y;
-    const int H = p.H[m], W = p.W[m], C = p.C[m], P = H * W;
-    const int n0 = t * HD_NT;
-    const float* f = p.feat[m] + (int64_t)b * P * C;
-    const float* wdw_g = p.w + p.dw_w[m];
-    const float* bdw_g = p.w + p.dw_b[m];
-    const float* wc_g = p.w + p.cw[m];
-    const int tid = threadIdx.x, nl = tid & 15, pg = tid >> 4;
-    f32x4 fr[HD_FQ];
-    float wr[HD_WQ], dr[HD_DQ];
-    auto load = [&](int c0) {
-#pragma unroll
-        for (int u = 0; u < HD_FQ; ++u) {
-            const int e = tid + 256 * u, px = e >> 3;  // 8 quads per pixel
-            fr[u] = px < P ? *reinterpret_cast<const f32x4*>(f + (int64_t)px * C + c0 + 4 * (e & 7))
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < HD_WQ; ++u) {
-            const int e = tid + 256 * u, nn = e / HD_CC;
-            wr[u] = n0 + nn < nout ? wc_g[(int64_t)(n0 + nn) * C + c0 + (e % HD_CC)] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < HD_DQ; ++u) {
-            const int e = tid + 256 * u;
-            dr[u] = e < 9 * HD_CC ? wdw_g[(int64_t)(e / HD_CC) * C + c0 + e % HD_CC]
-                                  : (e < 10 * HD_CC ? bdw_g[c0 + e - 9 * HD_CC] : 0.f);
-        }
-    };
-    float acc[HD_NO][HD_PQ];
-#pragma unroll
-    for (int k = 0; k < HD_NO; ++k)
-#pragma unroll
-        for (int q = 0; q < HD_PQ; ++q) acc[k][q] = 0.f;
-    load(0);
-    for (int c0 = 0; c0 < C; c0 += HD_CC) {
-        __syncthreads();  // the previous chunk's fs / ds / wc consumed
-#pragma unroll
-        for (int u = 0; u < HD_FQ; ++u) {
-            const int e = tid + 256 * u, px = e >> 3, j = 4 * (e & 7);
-            if (px < P) {
-                float* d = fs + px * (HD_CC + 1) + j;
-                d[0] = fr[u].x;
-                d[1] = fr[u].y;
-                d[2] = fr[u].z;
-                d[3] = fr[u].w;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < HD_WQ; ++u) {
-            const int e = tid + 256 * u;
-            wc[(e / HD_CC) * (HD_CC + 1) + e % HD_CC] = wr[u];
-        }
-#pragma unroll
-        for (int u = 0; u < HD_DQ; ++u) {
-            const int e = tid + 256 * u;
-            if (e < 10 * HD_CC) wdw[e] = dr[u];
-        }
-        if (c0 + HD_CC < C) load(c0 + HD_CC);  // in flight under this chunk's compute
-        __syncthreads();
-        for (int e = tid; e < P * HD_CC; e += 256) {
-            const int px = e / HD_CC, j = e - px * HD_CC;
-            const int y = px / W, x = px - y * W;
-            float a = 0.f;
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh) {
-                const int yy = y - 1 + kh;
-                if ((unsigned)yy >= (unsigned)H) continue;
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw) {
-                    const int xx = x - 1 + kw;
-                    if ((unsigned)xx >= (unsigned)W) continue;
-                    a = fmaf(fs[(yy * W + xx) * (HD_CC + 1) + j], wdw[(kh * 3 + kw) * HD_CC + j], a);
-                }
-            }
-            ds[px * (HD_CC + 1) + j] = apply_act(a + wdw[9 * HD_CC + j], ACT_RELU6);
-        }
-        __syncthreads();
-        for (int j = 0; j < HD_CC; ++j) {
-            float wv[HD_NO];
-#pragma unroll
-            for (int k = 0; k < HD_NO; ++k) wv[k] = wc[(nl + 16 * k) * (HD_CC + 1) + j];
-#pragma unroll
-            for (int q = 0; q < HD_PQ; ++q) {
-                const int px = pg + 16 * q;
-                if (px < P) {
-                    const float d = ds[px * (HD_CC + 1) + j];
-#pragma unroll
-                    for (int k = 0; k < HD_NO; ++k) acc[k][q] = fmaf(d, wv[k], acc[k][q]);
-                }
-            }
-        }
-    }
-    float* out = p.out + ((int64_t)(p.img0 + b) * p.A + p.a0[m]) * p.cols;
-#pragma unroll
-    for (int k = 0; k < HD_NO; ++k) {
-        const int nn = n0 + nl + 16 * k;
-        if (nn >= nout) continue;
-        const float bias = p.w[p.cb[m] + nn];
-#pragma unroll
-        for (int q = 0; q < HD_PQ; ++q) {
-            const int px = pg + 16 * q;
-            if (px < P) out[(int64_t)px * nout + nn] = acc[k][q] + bias;
-        }
-    }
-}
-
-int ssd_heads_launch(const SsdHeadsParams& p, hipStream_t s) {
-    EDGEDET_REQUIRE(p.w && p.out && p.nmaps >= 1 && p.nmaps <= 5 && p.cols >= 1 && p.B >= 1, "ssd_heads: bad arguments");
-    for (int m = 0; m < p.nmaps; ++m) {
-        EDGEDET_REQUIRE(p.feat[m], "ssd_heads: null feature map");
-        EDGEDET_REQUIRE(p.H[m] * p.W[m] <= HD_MAXP && p.C[m] % HD_CC == 0, "ssd_heads: maps <= 100 pixels, C % 32 == 0");
-        EDGEDET_REQUIRE(((uintptr_t)p.feat[m] & 15) == 0, "ssd_heads: feature maps 16-byte aligned");
-    }
-    const int ntiles = (6 * p.cols + HD_NT - 1) / HD_NT;
-    hipLaunchKernelGGL(ssd_heads_kernel, dim3((unsigned)(p.nmaps * ntiles), (unsigned)p.B), dim3(256), 0, s, p);
-    EDGEDET_LAUNCH_CHECK();
-    return 0;
-}
-
 int dwconv_launch(const DwParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");

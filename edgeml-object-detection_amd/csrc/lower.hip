@@ -483,8 +483,10 @@ static void conv_op(Plan& P, const ConvArgs& a) {
         }
     }
     const bool xf = a.in_scale.kind != Ref::NONE || a.in_shift.kind != Ref::NONE || a.in_relu;
-    const int presplit = env_int("EDGEDET_CONV_PRESPLIT", 1);
-    if (presplit != 0 && (xf || presplit == 2) && w3 && C % 32 == 0 && (o.i[23] == 0 || o.i[23] == 25))
+    // pre-split input planes only where an input transform is fused (GN / SE / ReLU on load): the split
+    // pass then also takes the per-element transform out of the GEMM loop; for a plain input the extra
+    // HBM pass measured slower (FRCNN 336 -> 313 img/s)
+    if (xf && w3 && C % 32 == 0 && (o.i[23] == 0 || o.i[23] == 25))
         o.p[8] = P.ref(P.x3_scratch(3 * B * H * W * C + 32));
     P.add(o);
 }
@@ -826,23 +828,6 @@ class SSDLite {
         int64_t off = 0;
         if (nch == 1) P.fork(3);
         int br = 0;
-        // EDGEDET_SSD_HEADS=1: maps 1..5 (10x10 and below) as one SSD_HEADS launch per branch.  Off by
-        // default: measured 23.7k against 27.3k img/s (r3e) — one workgroup walks its map's channels
-        // in 15 dependent chunks, so under the other chains' HBM traffic the launch takes ~250 us, where
-        // the ten separate depthwise + 1x1 launches each take one memory round trip.
-        const bool group = !pack_only && env_int("EDGEDET_SSD_HEADS", 0) == 1;
-        OpRec grp[2];
-        for (int h = 0; h < 2; ++h) {
-            grp[h].kind = EDGEDET_OP_SSD_HEADS;
-            grp[h].name = std::string(h == 0 ? "head.classification_head" : "head.regression_head") + ".maps1-5" + sfx;
-            grp[h].p[0] = Plan::wref(WRef{0, 0, -1});
-            grp[h].p[6] = P.ref(h == 0 ? sh.cls : sh.reg);
-            grp[h].i[0] = B;
-            grp[h].i[1] = (int64_t)feats.size() - 1;
-            grp[h].i[2] = A;
-            grp[h].i[3] = img0;
-            grp[h].i[4] = h == 0 ? NC : 4;
-        }
         for (size_t i = 0; i < feats.size(); ++i) {
             const Cur& f = feats[i];
             for (int h = 0; h < 2; ++h) {
@@ -850,17 +835,6 @@ class SSDLite {
                 const int64_t cols = h == 0 ? NC : 4;
                 const int out = h == 0 ? sh.cls : sh.reg;
                 const std::string p = "head." + name + ".module_list." + std::to_string(i);
-                if (group && i >= 1) {
-                    ConvW wd = cbn(p + ".0", f.s[3], f.s[3], 3, true);
-                    ConvW w = pk_.conv_bias(p + ".1.weight", p + ".1.bias", 6 * cols, f.s[3], 1);
-                    if (w.Kpad != f.s[3]) throw std::runtime_error("ssd heads: C must be a multiple of 32");
-                    OpRec& g = grp[h];
-                    const int m = (int)i - 1;
-                    g.p[1 + m] = f.x;
-                    const int64_t v[8] = {f.s[1], f.s[2], f.s[3], off, wd.w.off, wd.b.off, w.w.off, w.b.off};
-                    for (int j = 0; j < 8; ++j) g.i[5 + 8 * m + j] = v[j];
-                    continue;
-                }
                 if (nch == 1) P.lane(br % 4);
                 ++br;
                 DwOut t = dw(f, p + ".0", 3, 1, A_R6, false);
@@ -880,13 +854,6 @@ class SSDLite {
                 conv_op(P, a);
             }
             off += f.s[1] * f.s[2] * 6;
-        }
-        if (group) {
-            for (int h = 0; h < 2; ++h) {
-                if (nch == 1) P.lane(br % 4);
-                ++br;
-                P.add(grp[h]);
-            }
         }
         if (nch == 1) P.join();
         if (pack_only) return;
@@ -1162,7 +1129,6 @@ class ResNetFPN {
         cur = maxpool(P, cur, 3, 2, 1, "backbone.body.maxpool");
         // deep-K 3x3 convs on small maps fill the GPU only with split-K (tile 26), which cannot apply the
         // ReLU: conv3 then applies it to its input
-        const bool splitk_defer = env_int("EDGEDET_SPLITK_DEFER", 1) == 1;
         const char* lname[4] = {"layer1", "layer2", "layer3", "layer4"};
         const int nblk[4] = {3, 4, 6, 3}, width[4] = {64, 128, 256, 512}, lstride[4] = {1, 2, 2, 2};
         for (int L = 0; L < 4; ++L) {
@@ -1172,7 +1138,7 @@ class ResNetFPN {
                 const int wd = width[L];
                 Cur y = conv_bn(P, cur, q + "conv1.weight", q + "bn1", wd, 1, 1, A_RE);
                 const int64_t m = y.s[0] * ((y.s[1] - 1) / s + 1) * ((y.s[2] - 1) / s + 1);
-                const bool defer = splitk_defer && 9 * wd >= 2048 && ((m + 255) / 256) * ((wd + 127) / 128) < 200;
+                const bool defer = 9 * wd >= 2048 && ((m + 255) / 256) * ((wd + 127) / 128) < 200;
                 y = conv_bn(P, y, q + "conv2.weight", q + "bn2", wd, 3, s, defer ? A_NONE : A_RE);
                 Cur idn = bi == 0 ? conv_bn(P, cur, q + "downsample.0.weight", q + "downsample.1", wd * 4, 1, s, A_NONE)
                                   : cur;
@@ -1266,12 +1232,9 @@ class FasterRCNN : public ResNetFPN {
         const int Aa = 3;
         std::vector<std::pair<Ref, Ref>> heads;
         std::vector<std::pair<int, int>> grids;
-        // the five levels in order on the caller stream (EDGEDET_RPN_LANES=1: on four stream lanes, 0.75 %
-        // slower at two plans in flight, tools/gpu_r3ab.sh: eight streams over four hardware queues)
-        const bool rpn_lanes = env_int("EDGEDET_RPN_LANES", 0) == 1;
-        if (rpn_lanes) P.fork(3);
+        // the five levels in order on the caller stream (on four stream lanes measured 0.75 % slower at
+        // two plans in flight: eight streams over four hardware queues, round 3)
         for (size_t lvl = 0; lvl < outs.size(); ++lvl) {
-            if (rpn_lanes) P.lane((int)(lvl % 4));
             const std::string at = "@" + std::to_string(lvl);
             Cur t = conv_b(P, outs[lvl], "rpn.head.conv.0.0", 256, 3, 1, A_RE, "rpn.head.conv.0" + at);
             t = conv_b(P, t, "rpn.head.conv.1.0", 256, 3, 1, A_RE, "rpn.head.conv.1" + at);
@@ -1280,7 +1243,6 @@ class FasterRCNN : public ResNetFPN {
             heads.push_back({o.x, d.x});
             grids.push_back({(int)outs[lvl].s[1], (int)outs[lvl].s[2]});
         }
-        if (rpn_lanes) P.join();
         std::vector<int> anchor_bufs;
         const int sizes[5] = {32, 64, 128, 256, 512};
         for (size_t l = 0; l < grids.size(); ++l) {
@@ -1902,19 +1864,24 @@ extern "C" int edgedet_model_prepare(int32_t kind, int32_t num_classes, int32_t 
     Config c;
     if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
     EDGEDET_REQUIRE(workspace, "model_prepare: null workspace");
-    Plan* p = nullptr;
+    // what the workspace needs is copied out under the lock: once it is released another thread may
+    // evict (plan_for's LRU) or release (edgedet_model_release) the cached plan and free its host memory
+    int64_t arena = 0;
+    std::vector<std::pair<int64_t, std::vector<uint8_t>>> consts;
     EDGEDET_TRY({
         std::lock_guard<std::mutex> g(g_mu);
-        p = plan_for(engine(c), B, H, W, input_u8 != 0);
+        const Plan* p = plan_for(engine(c), B, H, W, input_u8 != 0);
+        arena = p->arena;
+        for (auto& kv : p->consts) consts.emplace_back(p->bufs[(size_t)kv.first].off, kv.second);
     })
     // zero first: every buffer starts from zero, as the Python host's arena does
-    EDGEDET_CHECK_HIP(hipMemsetAsync(workspace, 0, (size_t)p->arena, (hipStream_t)stream));
-    for (auto& kv : p->consts) {
-        char* dst = (char*)workspace + p->bufs[(size_t)kv.first].off;
+    EDGEDET_CHECK_HIP(hipMemsetAsync(workspace, 0, (size_t)arena, (hipStream_t)stream));
+    for (auto& kv : consts) {
+        char* dst = (char*)workspace + kv.first;
         EDGEDET_CHECK_HIP(hipMemcpyAsync(dst, kv.second.data(), kv.second.size(), hipMemcpyHostToDevice,
                                          (hipStream_t)stream));
     }
-    // the copies read pageable host memory owned by the cached plan: complete before returning
+    // the copies read this call's pageable host copies: complete before returning
     EDGEDET_CHECK_HIP(hipStreamSynchronize((hipStream_t)stream));
     return 0;
 }

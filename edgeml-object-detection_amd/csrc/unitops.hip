@@ -93,11 +93,23 @@ __global__ void nms_gather_kernel(const float* __restrict__ boxes, const int64_t
     }
 }
 
-// grid (column block cb, row block rb) with cb >= rb; one wave: lane = row rb*64 + lane
+// One workgroup per upper-triangle block (row block rb, column block cb >= rb): a 1-D grid of
+// nw * (nw + 1) / 2 blocks, row-major over the triangle (row rb starts at S(rb) = rb * nw - rb * (rb - 1) / 2).
+// One wave: lane = row rb*64 + lane.  (The lower triangle is never read: the scan uses words w >= b.)
+__device__ __forceinline__ void tri_block(int64_t t, int nw, int& rb, int& cb) {
+    const double a = 2.0 * nw + 1.0;
+    int64_t r = (int64_t)((a - sqrt(a * a - 8.0 * (double)t)) * 0.5);
+    auto S = [nw](int64_t q) { return q * nw - q * (q - 1) / 2; };
+    while (r > 0 && S(r) > t) --r;        // the double root can be off by one either way
+    while (r + 1 < nw && S(r + 1) <= t) ++r;
+    rb = (int)r;
+    cb = (int)(r + (t - S(r)));
+}
+
 __global__ void __launch_bounds__(64) nms_mask_kernel(const f32x4* __restrict__ sbox, const int64_t* __restrict__ sgrp,
                                                       int n, int nw, IouThr thr, unsigned long long* __restrict__ mask) {
-    const int cb = blockIdx.x, rb = blockIdx.y;
-    if (cb < rb) return;
+    int rb, cb;
+    tri_block((int64_t)blockIdx.x, nw, rb, cb);
     __shared__ f32x4 cbox[64];
     __shared__ float carea[64];
     __shared__ int64_t cgrp[64];
@@ -231,7 +243,7 @@ static int large_nms(const float* boxes, const float* scores, const int64_t* idx
     EDGEDET_CHECK_HIP(hipcub::DeviceRadixSort::SortPairsDescending(base + L.temp, tb, kin, kout, iin, iout, N, 0, 32, s));
     hipLaunchKernelGGL(nms_gather_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, s, boxes, idxs, iout, N, sbox, sgrp);
     EDGEDET_LAUNCH_CHECK();
-    hipLaunchKernelGGL(nms_mask_kernel, dim3((unsigned)nw, (unsigned)nw), dim3(64), 0, s, sbox, sgrp, N, nw,
+    hipLaunchKernelGGL(nms_mask_kernel, dim3((unsigned)((int64_t)nw * (nw + 1) / 2)), dim3(64), 0, s, sbox, sgrp, N, nw,
                        make_iou_thr(iou), mask);
     EDGEDET_LAUNCH_CHECK();
     hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(NMS_SCAN_NT), 0, s, mask, iout, N, nw, keep, d_num_keep);

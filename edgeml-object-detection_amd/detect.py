@@ -185,14 +185,16 @@ def main(opts):
     results = {}
     # Batches of equal-size images across the whole list (sizes from the file headers, no decode),
     # formed exactly as a single-process run forms them; under torchrun each rank takes a contiguous
-    # block of those batches, so outputs are independent of the GPU count.  Decoded by a thread pool
+    # block of those batches balanced by the model's per-batch work, so outputs are independent of the
+    # GPU count.  Decoded by a thread pool
     # one batch ahead of the engine (PIL releases the GIL while decoding).  Up to model.INFLIGHT
     # batches on the device at once (run_batches), so one batch's NMS tail overlaps the next
     # batch's backbone.
     sizes = image_sizes(dataset)
     clock.append(("sizes", time.perf_counter()))
     chunks = dist_mod.size_batches(sizes, batch)
-    shards = [dist_mod.batch_shard(chunks, r, world) for r in range(world)]
+    work = lambda c: model.batch_work(len(c), *sizes[c[0]])  # noqa: E731
+    shards = [dist_mod.batch_shard(chunks, r, world, work) for r in range(world)]
     shard_names = [[img_names[i] for c in sh for i in c] for sh in shards]
     my_names = shard_names[rank]
     tagged = (((names, hw), buf) for names, hw, buf in

@@ -85,16 +85,22 @@ def size_batches(sizes, batch):
     return [idx[k:k + batch] for idx in groups.values() for k in range(0, len(idx), batch)]
 
 
-def batch_shard(chunks, rank, world):
-    """A contiguous block of the batch list for `rank`, balanced by image count: batch j goes to
-    rank floor(c_j * world / N), c_j = the images in the batches before it.  Every batch lands on
-    exactly one rank, unchanged, so per-image results equal the world-1 run's bit for bit."""
-    n = sum(len(c) for c in chunks)
-    out, start = [], 0
-    for c in chunks:
-        if min(world - 1, start * world // max(n, 1)) == rank:
+def batch_shard(chunks, rank, world, cost=None):
+    """A contiguous block of the batch list for `rank`, balanced by work: batch j goes to rank
+    floor((W_j + w_j / 2) * world / W), where w_j = cost(batch j), W_j = the cost of the batches before
+    it and W the total (the batch's midpoint decides, so every rank's work is within one batch of
+    W / world).  cost=None counts images; the detect CLI passes the model's per-batch work (FRCNN /
+    RetinaNet: batch size x resized padded pixels, which vary up to 1.5x with the source size; SSDLite
+    resizes everything to 320 x 320, so its work is the image count).  Every batch lands on exactly
+    one rank, unchanged, so per-image results equal the world-1 run's bit for bit."""
+    w = [float(cost(c) if cost is not None else len(c)) for c in chunks]
+    total = sum(w)
+    out, start = [], 0.0
+    for c, wc in zip(chunks, w):
+        r = int((start + 0.5 * wc) * world // total) if total > 0 else 0
+        if min(world - 1, r) == rank:
             out.append(c)
-        start += len(c)
+        start += wc
     return out
 
 

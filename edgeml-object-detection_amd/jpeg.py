@@ -74,8 +74,10 @@ class PackedBatch:
 
 def batch_packets(paths, threads=0, pinned=True):
     """Entropy-decode a batch of JPEG files of one size on `threads` host threads in one library call
-    -> PackedBatch, or None when a file is not a JPEG the device path handles or the sizes differ (the
-    caller decodes the batch on the host).  Raises EdgeDetError on unreadable / corrupt files."""
+    -> PackedBatch, or None when a file is not a JPEG the device path handles — including a non-JPEG
+    file with a .jpg name and a JPEG whose entropy data the decoder rejects — or the sizes differ (the
+    caller decodes the batch on the host, as read_image would).  Raises EdgeDetError only on files
+    that cannot be opened or read."""
     import os
     L = ops.lib()
     n = len(paths)
@@ -109,6 +111,12 @@ def _nbytes(p):
     return int(p.numel()) if torch.is_tensor(p) else int(p.size)
 
 
+def packet_hw(pk):
+    """(H, W) of a host packet, from its header (csrc/jpeg.hip Header: magic, version, H, W, ...)."""
+    head = (pk[:16].numpy() if torch.is_tensor(pk) else np.asarray(pk[:16])).view(np.int32)
+    return int(head[2]), int(head[3])
+
+
 def plane_bytes(pk):
     return int(ops.lib().edgedet_jpeg_plane_bytes(pk.data_ptr() if torch.is_tensor(pk) else pk.ctypes.data))
 
@@ -140,6 +148,11 @@ class BatchDecoder:
         B, C, H, W = out.shape
         if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(packets) != B:
             raise ValueError("decode: out must be a contiguous cuda uint8 [B,3,H,W] tensor, one packet per image")
+        # the colour kernel indexes every image's planes with the batch's H, W: a packet of another size
+        # would make it read past that image's planes on the device
+        bad = [k for k, p in enumerate(packets) if packet_hw(p) != (H, W)]
+        if bad:
+            raise ValueError(f"decode: packet {bad[0]} is {packet_hw(packets[bad[0]])}, the batch is {(H, W)}")
         # device image: [offsets int64, padded to 256 B][packet 0][packet 1]... (each 256-B aligned);
         # numpy packets go through one pinned staging copy, pinned tensor packets are uploaded as they are
         head = (8 * B + 255) // 256 * 256

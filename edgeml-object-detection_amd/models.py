@@ -87,6 +87,11 @@ class _Detector:
             self._weights[key] = torch.from_numpy(self.blob).to(device)
         return self._weights[key]
 
+    def batch_work(self, B, H, W):
+        """Relative device work of one batch of B images of H x W (the detect CLI's shard balance,
+        distributed.batch_shard): proportional to the pixels the network runs on."""
+        return float(B)
+
     def build_plan(self, B, H, W, u8=False):
         """A new plan of (B, H, W, u8) on this model's device (CPU when none is set: records and
         constants only, for host-side checks)."""
@@ -343,6 +348,13 @@ class FasterRCNNFPNv2(_Detector):
         b = f32(f32(1.0) / f32(max(H, W))) * f32(self.MAX_SIZE)
         scale = float(min(a, b))
         return int(math.floor(H * scale)), int(math.floor(W * scale))
+
+    def batch_work(self, B, H, W):
+        """B x the resized image padded to /32 (GeneralizedRCNNTransform): FRCNN / RetinaNet cost
+        scales with those pixels (799 x 1199 is 1.5x 800 x 800)."""
+        h, w = self.resized_size(H, W)
+        d = self.DIVISIBLE
+        return float(B * (-(-h // d) * d) * (-(-w // d) * d))
 
     def attach(self, P):
         P.feats = [P.buffer(n) for n in ("backbone.fpn.layer_blocks.0.0.weight", "backbone.fpn.layer_blocks.1.0.weight",

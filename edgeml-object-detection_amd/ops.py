@@ -25,7 +25,6 @@ GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 SSD_STEM = 21
 MBCONV = 22
 WAIT = 23
-SSD_HEADS = 24
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)
@@ -197,7 +196,9 @@ def nms(boxes, scores, iou_threshold):
 
 
 def batched_nms(boxes, scores, idxs, iou_threshold):
-    """torchvision.ops.batched_nms on the device; result sorted by score desc, ties lower index."""
+    """torchvision.ops.batched_nms on the device; result sorted by score desc, ties lower index.
+    Scratch (edgedet_nms_workspace_size) grows quadratically in n: the IoU bitmask is
+    8 * n * ceil(n / 64) bytes (0.5 GB at n = 65,536; 34 GB at the 524,288 cap)."""
     _need_cuda(boxes, scores, idxs)
     n = int(scores.shape[0])
     keep = torch.empty(max(n, 1), dtype=torch.int64, device=scores.device)

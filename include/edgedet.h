@@ -69,8 +69,8 @@ enum {
     EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
     EDGEDET_OP_SSD_STEM = 21,     /* SSDLite features.0.0 + features.0.1 in one pass                  */
     EDGEDET_OP_MBCONV = 22,       /* InvertedResidual without SE: expand, depthwise, project, residual */
-    EDGEDET_OP_WAIT = 23,         /* lane i[0] waits for everything issued so far on lane i[1]         */
-    EDGEDET_OP_SSD_HEADS = 24     /* SSDLite head branch (dw3x3 + 1x1) of feature maps 1..5, one launch  */
+    EDGEDET_OP_WAIT = 23          /* lane i[0] waits for everything issued so far on lane i[1]         */
+    /* 24 is retired (round 3's grouped SSD head kernel, measured slower and removed) */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,
@@ -182,8 +182,13 @@ int edgedet_frcnn_forward(const void* weights, int32_t num_classes, const void* 
  * boxes [n,4], scores [n] -> keep [n] int64 (indices, score-descending, ties lower index first),
  * *d_num_keep int32.  Suppress j when inter/(area_i+area_j-inter) > iou_threshold.  n <= 524288:
  * up to 1024 boxes one workgroup does it all; above, a radix sort, a tiled IoU bitmask and a blocked
- * greedy scan (csrc/unitops.hip), with scratch from the stream-ordered allocator (hipMallocAsync on
- * `stream`); the _ws variants take caller-owned scratch of edgedet_nms_workspace_size(n) bytes instead.
+ * greedy scan (csrc/unitops.hip).  The scratch grows QUADRATICALLY with n: the IoU bitmask alone is
+ * 8 * n * ceil(n / 64) bytes (0.5 GB at n = 65,536; 34 GB at the 524,288 cap, which fits MI355X's
+ * 288 GB), plus about 40 bytes per box.  edgedet_nms / edgedet_batched_nms are CONVENIENCE entry
+ * points: they take that scratch from the stream-ordered allocator (hipMallocAsync on `stream`), so
+ * they allocate on the calling path.  The hot path (the model plans) never calls them; a caller that
+ * must not allocate uses the _ws variants with caller-owned scratch of edgedet_nms_workspace_size(n)
+ * bytes instead.
  */
 int edgedet_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
                 int64_t* keep, int32_t* d_num_keep, void* stream);

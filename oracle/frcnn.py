@@ -157,8 +157,14 @@ def box_postprocess(logits, deltas, proposals, image_shapes):
 class FasterRCNNOracle:
     """Callable with the torchvision detection-model contract (detect.py:78)."""
 
-    def __init__(self, state_dict, num_classes=91):
-        self.sd = {k: v.detach().to(torch.float32) if v.is_floating_point() else v
+    def __init__(self, state_dict, num_classes=91, dtype=torch.float32):
+        """dtype=torch.float64: the dense arithmetic (ResNet body, FPN, RPN head, box head and
+        predictor: every conv / linear, BatchNorm and activation) runs in float64, the ground truth
+        of bench.py's ORIE leg.  The transform, the proposal filter, MultiScaleRoIAlign (on the FPN
+        features rounded to float32) and the post-processing stay float32 as in the reference, on
+        float32-rounded inputs."""
+        self.dtype = dtype
+        self.sd = {k: v.detach().to(dtype) if v.is_floating_point() else v
                    for k, v in state_dict.items()}
         self.num_classes = num_classes
 
@@ -166,8 +172,9 @@ class FasterRCNNOracle:
     def forward_raw(self, images, hook=None):
         sd = _SD(self.sd)
         x, sizes = tv_ops.transform(list(images), MEAN, STD, MIN_SIZE, MAX_SIZE, divisible=DIVISIBLE)
-        feats = fpn(resnet_body(x, sd, hook), sd, hook)
-        props = rpn(feats, sd, sizes, tuple(x.shape[-2:]))
+        feats = fpn(resnet_body(x.to(self.dtype), sd, hook), sd, hook)
+        objs, dels, anchors = rpn_head(feats, sd, tuple(x.shape[-2:]))
+        props = rpn_filter([o.to(torch.float32) for o in objs], [d.to(torch.float32) for d in dels], anchors, sizes)
         logits, deltas = self.box_stage(feats, props, sizes, hook, sd)
         self.used_keys = sd.used
         return logits, deltas, props, sizes, feats
@@ -178,10 +185,11 @@ class FasterRCNNOracle:
         sd = _SD(self.sd) if sd is None else sd
         mh = max(s[0] for s in sizes)
         scales = [2.0 ** round(float(torch.tensor(f.shape[-2] / mh).log2())) for f in feats[:4]]
-        roi = tv_ops.multiscale_roi_align(feats[:4], props, scales)
+        roi = tv_ops.multiscale_roi_align([f.to(torch.float32) for f in feats[:4]], props, scales)
         if hook is not None:
             hook("__roi_features__", roi)
-        return box_head(roi, sd, hook)
+        logits, deltas = box_head(roi.to(self.dtype), sd, hook)
+        return logits.to(torch.float32), deltas.to(torch.float32)
 
     @torch.no_grad()
     def rpn_raw(self, feats, padded_size):

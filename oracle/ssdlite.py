@@ -179,8 +179,13 @@ def postprocess(cls_logits, bbox_reg, anchors, num_classes):
 class SSDLiteOracle:
     """Callable with the torchvision detection-model contract (detect.py:78)."""
 
-    def __init__(self, state_dict, num_classes=91, reduced_tail=None):
-        self.sd = {k: v.detach().to(torch.float32) if v.is_floating_point() else v
+    def __init__(self, state_dict, num_classes=91, reduced_tail=None, dtype=torch.float32):
+        """dtype=torch.float64: the convolutions, BatchNorm, activations and SE of the backbone and
+        head run in float64 (the higher-precision ground truth of bench.py's ORIE leg); the
+        transform before them and the post-processing after them stay float32 as in the reference,
+        on the head outputs rounded to float32."""
+        self.dtype = dtype
+        self.sd = {k: v.detach().to(dtype) if v.is_floating_point() else v
                    for k, v in state_dict.items()}
         if reduced_tail is None:
             reduced_tail = self.sd["backbone.features.1.3.0.weight"].shape[1] == 80
@@ -193,8 +198,9 @@ class SSDLiteOracle:
         """images: list/tensor of [3,H,W] float32 in [0,1] -> (cls_logits, bbox_reg, sizes)."""
         sd = _SD(self.sd)
         x, sizes = tv_ops.transform(list(images), [0.5] * 3, [0.5] * 3, 320, 320, fixed=SIZE)
-        feats = backbone(x, sd, self.reduced_tail, hook)
+        feats = backbone(x.to(self.dtype), sd, self.reduced_tail, hook)
         cls, reg = head(feats, sd, self.num_classes, hook)
+        cls, reg = cls.to(torch.float32), reg.to(torch.float32)
         if self.anchors is None:
             self.anchors = tv_ops.ssd_default_boxes([f.shape[-2:] for f in feats], SIZE)
         self.used_keys = sd.used

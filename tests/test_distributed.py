@@ -72,6 +72,32 @@ def test_size_batches_and_batch_shard():
                 assert max(load) - min(load) <= 2 * batch
 
 
+def test_batch_shard_balances_frcnn_work_on_coco_sizes():
+    """A 5,000-image COCO-size list at world 8 with the FRCNN batches of the detect CLI: balanced by
+    the model's batch work (batch x resized padded pixels, models.FasterRCNNFPNv2.batch_work), every
+    rank's work is within one batch of the ideal share; the world-1 batches are unchanged and the
+    blocks contiguous.  Balancing by image count instead leaves a larger spread on the same list."""
+    from edgeml_amd import distributed as D
+    from edgeml_amd.models import FasterRCNNFPNv2
+    m = object.__new__(FasterRCNNFPNv2)  # batch_work needs only the class's transform constants
+    rs = np.random.RandomState(1)
+    # COCO val2017's common shapes (640 on the long side, portrait and landscape), mixed by frequency
+    pool = [(480, 640), (427, 640), (640, 480), (425, 640), (640, 427), (424, 640), (428, 640),
+            (612, 612), (500, 375), (375, 500), (333, 500), (640, 640), (360, 640), (640, 360)]
+    p = np.array([20, 14, 9, 8, 6, 5, 5, 3, 3, 3, 3, 3, 2, 2], float)
+    sizes = [pool[k] for k in rs.choice(len(pool), 5000, p=p / p.sum())]
+    batch, world = m.max_batch, 8
+    chunks = D.size_batches(sizes, batch)
+    work = lambda c: m.batch_work(len(c), *sizes[c[0]])  # noqa: E731
+    parts = [D.batch_shard(chunks, r, world, work) for r in range(world)]
+    assert sum(parts, []) == chunks
+    load = [sum(work(c) for c in part) for part in parts]
+    ideal, wmax = sum(load) / world, max(work(c) for c in chunks)
+    assert all(abs(x - ideal) <= wmax for x in load), (load, ideal, wmax)
+    by_count = [sum(work(c) for c in D.batch_shard(chunks, r, world)) for r in range(world)]
+    assert max(load) - min(load) <= max(by_count) - min(by_count)
+
+
 @pytest.mark.parametrize("n,batched", [(7, False), (1, False), (11, True)])
 def test_gather_rows_world2(n, batched):
     names = [f"{i:06d}" for i in range(n)]

@@ -69,6 +69,33 @@ def test_gpu_decode_synthetic_coco_set(tmp_path):
             np.testing.assert_array_equal(out[b].cpu().numpy(), ref)
 
 
+def _corrupt_scan_copy(src, dst):
+    """Copy a baseline JPEG with bytes of its entropy-coded scan overwritten so that the device path's
+    entropy decoder rejects it (edgedet_jpeg_packet raises) while PIL/libjpeg still decodes it."""
+    from edgeml_amd import jpeg, ops
+    data = bytearray(src.read_bytes())
+    sos = data.index(b"\xff\xda")
+    start = sos + 2 + int.from_bytes(data[sos + 2:sos + 4], "big")
+    rs = np.random.RandomState(0)
+    for _ in range(200):
+        d = bytearray(data)
+        at = int(rs.randint(start + 64, len(d) - 256))
+        d[at:at + 24] = bytes(int(v) for v in rs.randint(0, 255, 24))  # no 0xFF: no new markers
+        try:
+            jpeg.packet(bytes(d))
+            continue  # still parses: try another spot
+        except ops.EdgeDetError:
+            pass
+        try:
+            with Image.open(io.BytesIO(bytes(d))) as im:
+                im.convert("RGB").load()
+        except Exception:
+            continue
+        dst.write_bytes(bytes(d))
+        return
+    raise AssertionError("no corruption found that the device decoder rejects and PIL decodes")
+
+
 def test_detect_cli_gpu_decode_equals_host_decode(tmp_path):
     """The detect CLI with the device JPEG path (default) writes byte-identical .npy files to the
     all-host decode (--decode host): mixed sizes, a ragged batch, and a PNG among the JPEGs (its
@@ -77,14 +104,19 @@ def test_detect_cli_gpu_decode_equals_host_decode(tmp_path):
     from edgeml_amd import detect, synthetic
     img = tmp_path / "imgs"
     names = synthetic.make_dataset(str(img), 11, seed=4, ext=".jpg", sizes=[(480, 640), (427, 640)])
-    synthetic.make_dataset(str(tmp_path / "png"), 1, seed=8, ext=".png", sizes=[(480, 640)])
+    synthetic.make_dataset(str(tmp_path / "png"), 2, seed=8, ext=".png", sizes=[(480, 640)])
     os.replace(tmp_path / "png" / "000000000000.png", img / "zz_extra.png")
+    # a PNG saved under a .jpg name (read_image picks the format from the magic bytes) and a JPEG
+    # whose scan the device path's entropy decoder rejects (libjpeg warns and still decodes): their
+    # batches fall back to the host decoder instead of failing the run
+    os.replace(tmp_path / "png" / "000000000001.png", img / "zz_png_named.jpg")
+    _corrupt_scan_copy(img / (names[0] + ".jpg"), img / "zz_corrupt.jpg")
     outs = {}
     for mode in ("gpu", "host"):
         d = tmp_path / mode
         detect.main(detect.getargs([str(img), str(d), "--decode", mode]))
         outs[mode] = d
     files = sorted(os.listdir(outs["gpu"]))
-    assert files == sorted(os.listdir(outs["host"])) and len(files) == len(names) + 1
+    assert files == sorted(os.listdir(outs["host"])) and len(files) == len(names) + 3
     for f in files:
         assert (outs["gpu"] / f).read_bytes() == (outs["host"] / f).read_bytes(), f

@@ -163,10 +163,7 @@ def test_ssd_plan_lowering():
     # two convs fewer each
     mb = kinds.count(ops.MBCONV)
     assert mb == (0 if os.environ.get("EDGEDET_MB_BLOCK") == "0" else 2)
-    # the head branches of maps 1..5 as one SSD_HEADS op per branch (10 depthwise + 10 convs fewer)
-    grouped = os.environ.get("EDGEDET_SSD_HEADS") == "1"
-    assert kinds.count(ops.SSD_HEADS) == (2 if grouped else 0)
-    heads = 2 if grouped else 12
+    heads = 12
     assert n_dw == 15 + 4 + heads - stem - mb
     assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + heads - 2 * stem - 2 * mb
     assert kinds.count(ops.SE_FC) == 8

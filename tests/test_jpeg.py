@@ -167,9 +167,14 @@ def test_batch_packets_equal_per_file_packets(tmp_path):
     other = tmp_path / "other.jpg"
     other.write_bytes(_encode(_scene(64, 128, 1)))
     assert jpeg.batch_packets(paths[:2] + [str(other)], 2, pinned=False) is None  # sizes differ
+    # files the decoder rejects make the batch "unsupported" (decoded on the host, as read_image
+    # would): malformed headers, a PNG saved under a .jpg name, corrupt entropy data
     bad = tmp_path / "bad.jpg"
     bad.write_bytes(b"\xff\xd8\xff\xdb" + bytes(40))
-    with pytest.raises(ops.EdgeDetError):
-        jpeg.batch_packets(paths[:2] + [str(bad)], 2, pinned=False)
+    assert jpeg.batch_packets(paths[:2] + [str(bad)], 2, pinned=False) is None
+    png = tmp_path / "png.jpg"
+    _scene(96, 128, 3).save(png, format="PNG")
+    assert jpeg.batch_packets(paths[:2] + [str(png)], 2, pinned=False) is None
+    assert "rejected" in ops.lib().edgedet_last_error().decode()
     with pytest.raises(ops.EdgeDetError):
         jpeg.batch_packets([str(tmp_path / "missing.jpg")], 1, pinned=False)

@@ -112,11 +112,15 @@ def main():
         got = z["reward"]
     ref = orie.orie_all(sub["weak_o"], sub["strong_o"], sub["labels"], E, seed=1000)
     d = np.abs(got - ref)
-    same_rows = sum(np.load(os.path.join(sub["weak_g"], n[:-4] + ".npy")).tobytes() ==
-                    np.load(os.path.join(sub["weak_o"], n[:-4] + ".npy")).tobytes() for n in names)
     print(f"ORIE subset parity: {len(names)} images, E={E}: max |dORIE| = {d.max():.3e}, "
-          f"{int(np.count_nonzero(d))} images differ, {int(np.count_nonzero(ref))} nonzero oracle ORIE; "
-          f"weak files byte-identical for {same_rows}/{len(names)} images", flush=True)
+          f"{int(np.count_nonzero(d))} images differ, {int(np.count_nonzero(ref))} nonzero oracle ORIE", flush=True)
+    # identity-paired file differences (rows paired by class and IoU >= 0.99, tools/rowpair.py)
+    from tools import rowpair
+    stems = [n[:-4] for n in names]
+    for det in ("weak", "strong"):
+        r = rowpair.compare_dirs(stems, lambda s_: np.load(os.path.join(sub[det + "_g"], s_ + ".npy")),
+                                 lambda s_: np.load(os.path.join(sub[det + "_o"], s_ + ".npy")))
+        print(f"{det} files engine vs oracle: {r}", flush=True)
 
 
 if __name__ == "__main__":
