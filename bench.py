@@ -280,7 +280,7 @@ def op_work(op):
         B, H, W, Cin, Cexp, Cout, Ho, Wo, K = (i[j] for j in range(9))
         fl = 2.0 * B * (H * W * Cin * Cexp + Ho * Wo * Cexp * (K * K + Cout))
         return "mbconv", fl, 4.0 * (B * H * W * Cin + B * Ho * Wo * Cout + Cexp * (Cin + K * K + Cout + 2) + Cout)
-    if k in (O.FORK, O.JOIN, O.WAIT):
+    if k in (O.FORK, O.JOIN, O.WAIT, O.GROUP):
         return "lanes", 0.0, 0.0
     if k == O.MEMSET:  # zeroing the output of a split-K conv
         return "conv", 0.0, float(i[0])
@@ -299,8 +299,8 @@ def per_op_times(plan, stream, reps=20):
     recs["i"][:, O.LANE_FIELD] = 0  # time every op alone on the timed stream
     with torch.cuda.stream(stream):
         for k in range(len(recs)):
-            if recs[k]["kind"] in (O.FORK, O.JOIN, O.WAIT):
-                res.append(0.0)
+            if recs[k]["kind"] in (O.FORK, O.JOIN, O.WAIT, O.GROUP):
+                res.append(0.0)  # a GROUP's members are timed one by one (each alone)
                 continue
             ptr = recs[k:k + 1].ctypes.data_as(ctypes.c_void_p)
             O.check(L.edgedet_plan_run(ptr, 1, sh))

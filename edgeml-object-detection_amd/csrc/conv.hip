@@ -859,7 +859,7 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // BN = 64 (with BM = 128, the skewed 16x16x32 pipeline and LDS-DMA B only): 4 x 2 waves of 32 x 32
 // for the Cout = 64 layers, which a 128-wide N tile computes half empty; waves 0..3 copy the B rows.
 template <bool XF, bool UT, bool PS, int BM = 256, int PF = 1, bool P1 = false, int BN = 128>
-__global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
+__device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
     static_assert(!P1 || !PS, "pointwise stages: fp32 input");
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
     const int nnt = (p.Cout + BN - 1) / BN;
     const int nwg = nmt * nnt;
     const int ksp = p.ksplit > 1 ? 2 : 1;  // split-K: block 2t + s takes K half s of tile t
-    int bid = blockIdx.x / ksp;
+    int bid = blk / ksp;
     {
         const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
@@ -1084,8 +1084,8 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
     };
 
     const int nk_all = p.Kpad / BK6B;
-    const int kbeg = ksp > 1 ? (blockIdx.x & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
-    const int nk = ksp > 1 ? ((blockIdx.x & 1) ? nk_all - kbeg : (nk_all + 1) / 2) : nk_all;
+    const int kbeg = ksp > 1 ? (blk & 1) * ((nk_all + 1) / 2) : 0;  // stage range of this block
+    const int nk = ksp > 1 ? ((blk & 1) ? nk_all - kbeg : (nk_all + 1) / 2) : nk_all;
     // Stage order. Tap-major (stage s at k = 32 s, the weight layout) sweeps a block's whole input
     // panel once per filter tap; with a uniform tap the stages run channel-chunk-major instead (the
     // KH*KW taps of one 32-channel chunk back to back, k = tap * Cin + 32 * chunk; K = KH*KW*Cin is
@@ -1253,6 +1253,23 @@ __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_ke
     conv_epilogue<TM, TN, true>(p, acc, m0 + wave_m * TM * 32, n0 + wave_n * TN * 32, h, l32);
 }
 
+// The kernel of one conv problem, and the grouped form (csrc/exec.hip EDGEDET_OP_GROUP): one launch
+// over up to EDGEDET_MAX_GROUP independent problems of the same tile and template variant (e.g. the
+// twelve SSDLite head 1x1 convs), workgroup ranges [g.start[k], g.start[k+1]) running problem k with
+// its own XCD-aware block order.
+template <bool XF, bool UT, bool PS, int BM = 256, int PF = 1, bool P1 = false, int BN = 128>
+__global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
+    conv_x6b_body<XF, UT, PS, BM, PF, P1, BN>(p, (int)blockIdx.x);
+}
+
+template <bool XF, bool UT, int BM, bool P1, int BN>
+__global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_group_kernel(ConvGroup g) {
+    const int bx = (int)blockIdx.x;
+    int k = 0;
+    while (k + 1 < g.n && bx >= g.start[k + 1]) ++k;  // uniform: scalar loads of the range table
+    conv_x6b_body<XF, UT, false, BM, 1, P1, BN>(g.p[k], bx - g.start[k]);
+}
+
 // Pre-split of a conv input for the PS tile: out[pl][pix][c] (three dense bf16 planes, the RN split
 // of split3_bf16) of transform(x[pix][c]); 8 channels per thread, a grid-stride pass.  HBM-bound:
 // 4 B read + 6 B written per element.
@@ -1315,6 +1332,33 @@ static int launch_x6b(const ConvParams& p0, hipStream_t s) {
          : xf ? (ut ? conv_x6b_kernel<true, true, false, BM, PF, false, BN> : conv_x6b_kernel<true, false, false, BM, PF, false, BN>)
               : (ut ? conv_x6b_kernel<false, true, false, BM, PF, false, BN> : conv_x6b_kernel<false, false, false, BM, PF, false, BN>);
     hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(512), 0, s, p);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int BM, int BN>
+static int launch_x6b_group(ConvGroup& g, hipStream_t s) {
+    const ConvParams& p = g.p[0];
+    const bool xf = p.in_scale || p.in_shift || p.in_relu, ut = p.Cin % BK6B == 0;
+    const bool p1 = p.lin_x && p.KH == 1 && p.KW == 1 && p.Cin % 4 == 0;
+    int64_t total = 0;
+    for (int k = 0; k < g.n; ++k) {
+        const ConvParams& q = g.p[k];
+        EDGEDET_REQUIRE(q.w3 && ((uintptr_t)q.w3 & 15) == 0 && q.Kpad % BK6B == 0 && q.ksplit <= 1,
+                        "conv group: bf16x6 members with 16-byte aligned split planes, Kpad % 32 == 0, no split-K");
+        const bool qxf = q.in_scale || q.in_shift || q.in_relu, qut = q.Cin % BK6B == 0;
+        const bool qp1 = q.lin_x && q.KH == 1 && q.KW == 1 && q.Cin % 4 == 0;
+        EDGEDET_REQUIRE(qxf == xf && qut == ut && qp1 == p1, "conv group: members of one kernel variant");
+        g.start[k] = (int)total;
+        total += cdiv(q.M, BM) * cdiv(q.Cout, BN);
+        EDGEDET_REQUIRE(total < (1ll << 31), "conv group grid too large");
+    }
+    g.start[g.n] = (int)total;
+    auto k = p1 ? (xf ? (ut ? conv_x6b_group_kernel<true, true, BM, true, BN> : conv_x6b_group_kernel<true, false, BM, true, BN>)
+                      : (ut ? conv_x6b_group_kernel<false, true, BM, true, BN> : conv_x6b_group_kernel<false, false, BM, true, BN>))
+         : xf ? (ut ? conv_x6b_group_kernel<true, true, BM, false, BN> : conv_x6b_group_kernel<true, false, BM, false, BN>)
+              : (ut ? conv_x6b_group_kernel<false, true, BM, false, BN> : conv_x6b_group_kernel<false, false, BM, false, BN>);
+    hipLaunchKernelGGL(k, dim3((unsigned)total), dim3(512), 0, s, g);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -1542,6 +1586,31 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
             EDGEDET_REQUIRE(p.lin_x, "pw tiles need a 1x1/stride-1 dense input");
             return launch_pw_splitk<2>(p, s);           // split-K over 4 waves, 32 x 64
         default: EDGEDET_REQUIRE(false, "conv: unknown tile config");
+    }
+}
+
+// Grouped launch of up to EDGEDET_MAX_GROUP conv problems (exec.hip EDGEDET_OP_GROUP).  Every member
+// must resolve to the same x6b tile (29 / 31 / 38 / 25, no pre-split input) and kernel variant; returns
+// 1 without launching when they do not, and the caller then issues them one by one.
+int conv_group_launch(const ConvParams* ps, int n, int tile, hipStream_t s) {
+    EDGEDET_REQUIRE(n >= 1 && n <= EDGEDET_MAX_GROUP, "conv group: 1..EDGEDET_MAX_GROUP members");
+    ConvGroup gl;  // about 3 KB, passed by value as the kernel's argument block
+    gl.n = n;
+    int t0 = -1;
+    for (int k = 0; k < n; ++k) {
+        gl.p[k] = ps[k];
+        const int rc = conv_prepare(gl.p[k]);
+        if (rc) return rc;
+        const int t = conv_resolve_tile(gl.p[k], tile);
+        if (k == 0) t0 = t;
+        if (t != t0 || gl.p[k].x3) return 1;
+    }
+    switch (t0) {
+        case 25: return launch_x6b_group<256, 128>(gl, s);
+        case 29: return launch_x6b_group<128, 128>(gl, s);
+        case 31: return launch_x6b_group<64, 128>(gl, s);
+        case 38: return launch_x6b_group<128, 64>(gl, s);
+        default: return 1;
     }
 }
 

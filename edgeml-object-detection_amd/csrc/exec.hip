@@ -127,6 +127,29 @@ static ConvParams conv_params(const edgedet_op& o) {
     return p;
 }
 
+// DWCONV record -> DwParams.
+static DwParams dw_params(const edgedet_op& o) {
+    const int64_t* I = o.i;
+    DwParams p{};
+    p.x = P<const float>(o, 0);
+    p.w = P<const float>(o, 1);
+    p.bias = P<const float>(o, 2);
+    p.y = P<float>(o, 3);
+    p.part = P<float>(o, 4);
+    p.B = (int)I[0];
+    p.H = (int)I[1];
+    p.W = (int)I[2];
+    p.C = (int)I[3];
+    p.Ho = (int)I[4];
+    p.Wo = (int)I[5];
+    p.K = (int)I[6];
+    p.stride = (int)I[7];
+    p.pad = (int)I[8];
+    p.act = (int)I[9];
+    p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
+    return p;
+}
+
 // Diagnostic only (wrong results), compiled in only with -DEDGEDET_DIAG (never in the product
 // library): EDGEDET_DIAG_SKIP=k1,k2,... launches nothing for ops of those kinds (100 + t: convs whose
 // requested tile is t), to measure what each op family costs the steady-state step under stream
@@ -217,26 +240,8 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             EDGEDET_REQUIRE(p.K == p.KH * p.KW * p.Cin, "conv: K != KH*KW*Cin");
             return conv_launch(p, (int)I[23], s);
         }
-        case EDGEDET_OP_DWCONV: {
-            DwParams p{};
-            p.x = P<const float>(o, 0);
-            p.w = P<const float>(o, 1);
-            p.bias = P<const float>(o, 2);
-            p.y = P<float>(o, 3);
-            p.part = P<float>(o, 4);
-            p.B = (int)I[0];
-            p.H = (int)I[1];
-            p.W = (int)I[2];
-            p.C = (int)I[3];
-            p.Ho = (int)I[4];
-            p.Wo = (int)I[5];
-            p.K = (int)I[6];
-            p.stride = (int)I[7];
-            p.pad = (int)I[8];
-            p.act = (int)I[9];
-            p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
-            return dwconv_launch(p, s);
-        }
+        case EDGEDET_OP_DWCONV:
+            return dwconv_launch(dw_params(o), s);
         case EDGEDET_OP_CHANNEL_MEAN:
             return channel_mean_launch(P<const float>(o, 0), P<float>(o, 1), (int)I[0], (int)I[1], (int)I[2], s);
         case EDGEDET_OP_SE_FC:
@@ -534,6 +539,18 @@ static int64_t check_topology(const edgedet_op* ops, int64_t n) {
             EDGEDET_REQUIRE(a >= 0 && b >= 0 && a != b && a <= forked && b <= forked,
                             at + "wait: two distinct forked lanes");
             ++waits;
+        } else if (o.kind == EDGEDET_OP_GROUP) {
+            // the next i0 records: all CONV or all DWCONV, on the GROUP record's lane
+            const int64_t g = o.i[0], lane = o.i[EDGEDET_OP_LANE];
+            EDGEDET_REQUIRE(g >= 1 && g <= EDGEDET_MAX_GROUP && k + g < n, at + "group: 1..12 following records");
+            EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
+                            at + "group on a lane that is not forked");
+            const int64_t kind = ops[k + 1].kind;
+            EDGEDET_REQUIRE(kind == EDGEDET_OP_CONV || kind == EDGEDET_OP_DWCONV, at + "group: CONV or DWCONV members");
+            for (int64_t j = k + 1; j <= k + g; ++j)
+                EDGEDET_REQUIRE(ops[j].kind == kind && ops[j].i[EDGEDET_OP_LANE] == lane,
+                                at + "group: members of one kind on the group's lane");
+            k += g;
         } else {
             const int64_t lane = o.i[EDGEDET_OP_LANE];
             EDGEDET_REQUIRE(lane >= 0 && lane < EDGEDET_MAX_LANES && (lane == 0 || lane <= forked),
@@ -542,6 +559,31 @@ static int64_t check_topology(const edgedet_op* ops, int64_t n) {
     }
     EDGEDET_REQUIRE(forked == 0, "plan ends with side lanes still forked (missing JOIN)");
     return waits;
+}
+
+// A GROUP's members as one grouped launch (conv_group_launch / dwconv_group_launch); members that
+// cannot share a kernel variant are issued one by one (same results, more launches).
+static int run_group(const edgedet_op* m, int n, hipStream_t s) {
+    int rc = 1;
+    if (diag_skip_mask() >> (m[0].kind & 63) & 1) return 0;
+    if (m[0].kind == EDGEDET_OP_CONV) {
+        ConvParams ps[EDGEDET_MAX_GROUP];
+        for (int k = 0; k < n; ++k) {
+            ps[k] = conv_params(m[k]);
+            EDGEDET_REQUIRE(ps[k].K == ps[k].KH * ps[k].KW * ps[k].Cin, "conv: K != KH*KW*Cin");
+        }
+        rc = conv_group_launch(ps, n, (int)m[0].i[23], s);
+    } else {
+        DwParams ps[EDGEDET_MAX_GROUP];
+        for (int k = 0; k < n; ++k) ps[k] = dw_params(m[k]);
+        rc = dwconv_group_launch(ps, n, s);
+    }
+    if (rc <= 0) return rc;
+    for (int k = 0; k < n; ++k) {
+        const int r = run_op(m[k], s);
+        if (r) return r;
+    }
+    return 0;
 }
 
 static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
@@ -573,6 +615,9 @@ static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
             hipEvent_t e = lanes->wait_ev[(size_t)wait_k++];
             EDGEDET_CHECK_HIP(hipEventRecord(e, lane_stream(o.i[1])));
             EDGEDET_CHECK_HIP(hipStreamWaitEvent(lane_stream(o.i[0]), e, 0));
+        } else if (o.kind == EDGEDET_OP_GROUP) {
+            rc = run_group(ops + k + 1, (int)o.i[0], lane_stream(o.i[EDGEDET_OP_LANE]));
+            k += o.i[0];
         } else {
             rc = run_op(o, lane_stream(o.i[EDGEDET_OP_LANE]));
         }

@@ -28,6 +28,15 @@ struct ConvParams {
     FastDiv div_howo, div_wo, div_cin, div_kw;
 };
 
+// Up to EDGEDET_MAX_GROUP conv problems issued as one launch (conv_group_launch): problem k runs the
+// workgroups [start[k], start[k + 1]).
+struct ConvGroup {
+    int n;
+    int start[EDGEDET_MAX_GROUP + 1];
+    ConvParams p[EDGEDET_MAX_GROUP];
+};
+int conv_group_launch(const ConvParams* ps, int n, int tile, hipStream_t s);
+
 struct PreParams {
     const float* x;      // [B][3][H][W] float in [0, 1] (the model contract, detect.py:78), or
     const uint8_t* xu8;  // [B][3][H][W] the decoded uint8 image (detect.py:57); x / 255 on the device
@@ -46,6 +55,15 @@ struct DwParams {
     int B, H, W, C, Ho, Wo, K, stride, pad, act;
     int parts;       // pixel splits of the squeeze (1..SE_PARTS)
 };
+
+// Up to EDGEDET_MAX_GROUP depthwise problems issued as one launch (dwconv_group_launch).
+struct DwGroup {
+    int n;
+    int start[EDGEDET_MAX_GROUP + 1];
+    int nq[EDGEDET_MAX_GROUP], nwg[EDGEDET_MAX_GROUP];
+    DwParams p[EDGEDET_MAX_GROUP];
+};
+int dwconv_group_launch(const DwParams* ps, int n, hipStream_t s);
 
 // A whole InvertedResidual without SqueezeExcitation (csrc/layers.hip mbconv_kernel).
 struct MbParams {

@@ -217,8 +217,7 @@ __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restr
 }
 
 template <int K, int S, int PW>
-__global__ void __launch_bounds__(256) dwconv_rb_kernel(DwParams p, int nq, int nwg) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void dwconv_rb_body(const DwParams& p, int nq, int nwg, int64_t idx) {
     const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
     if (idx >= total) return;
     const int q = (int)(idx % nq);
@@ -244,6 +243,22 @@ __global__ void __launch_bounds__(256) dwconv_rb_kernel(DwParams p, int nq, int 
             *reinterpret_cast<f32x4*>(yb + (int64_t)o * p.C) = v;
         }
     }
+}
+
+template <int K, int S, int PW>
+__global__ void __launch_bounds__(256) dwconv_rb_kernel(DwParams p, int nq, int nwg) {
+    dwconv_rb_body<K, S, PW>(p, nq, nwg, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Grouped form (csrc/exec.hip EDGEDET_OP_GROUP): up to EDGEDET_MAX_GROUP depthwise problems of one
+// (K, stride) in one launch (the twelve SSDLite head depthwise convs); workgroups [start[k], start[k+1])
+// run problem k.
+template <int K, int S, int PW>
+__global__ void __launch_bounds__(256) dwconv_rb_group_kernel(DwGroup g) {
+    const int bx = (int)blockIdx.x;
+    int k = 0;
+    while (k + 1 < g.n && bx >= g.start[k + 1]) ++k;
+    dwconv_rb_body<K, S, PW>(g.p[k], g.nq[k], g.nwg[k], (int64_t)(bx - g.start[k]) * blockDim.x + threadIdx.x);
 }
 
 template <int K, int S, int PW>
@@ -777,6 +792,35 @@ int mbconv_launch(const MbParams& p, hipStream_t s) {
     if (p.K == 5 && p.stride == 1) return mbconv_launch_ks<5, 1>(p, s);
     if (p.K == 5 && p.stride == 2) return mbconv_launch_ks<5, 2>(p, s);
     EDGEDET_REQUIRE(false, "mbconv: K in {3, 5}, stride in {1, 2}");
+}
+
+// Grouped launch of depthwise problems (exec.hip EDGEDET_OP_GROUP): every member a register-blocked
+// shape (K 3 / 5, stride 1 / 2) of one (K, stride), no SE squeeze; returns 1 without launching when
+// they are not, and the caller issues them one by one.
+int dwconv_group_launch(const DwParams* ps, int n, hipStream_t s) {
+    EDGEDET_REQUIRE(n >= 1 && n <= EDGEDET_MAX_GROUP, "dwconv group: 1..EDGEDET_MAX_GROUP members");
+    constexpr int PW = 4;
+    DwGroup g;
+    g.n = n;
+    const int K = ps[0].K, S = ps[0].stride;
+    int64_t total = 0;
+    for (int k = 0; k < n; ++k) {
+        const DwParams& p = ps[k];
+        EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y && p.C % 4 == 0, "dwconv group: null pointer or C % 4 != 0");
+        if (p.K != K || p.stride != S || p.part || !((K == 3 || K == 5) && (S == 1 || S == 2))) return 1;
+        g.p[k] = p;
+        g.nq[k] = p.C / 4;
+        g.nwg[k] = cdiv(p.Wo, PW);
+        g.start[k] = (int)total;
+        total += cdiv((int64_t)p.B * p.Ho * g.nwg[k] * g.nq[k], 256);
+        EDGEDET_REQUIRE(total < (1ll << 31), "dwconv group grid too large");
+    }
+    g.start[n] = (int)total;
+    auto kern = K == 3 ? (S == 1 ? dwconv_rb_group_kernel<3, 1, PW> : dwconv_rb_group_kernel<3, 2, PW>)
+                       : (S == 1 ? dwconv_rb_group_kernel<5, 1, PW> : dwconv_rb_group_kernel<5, 2, PW>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)total), dim3(256), 0, s, g);
+    EDGEDET_LAUNCH_CHECK();
+    return 0;
 }
 
 int dwconv_launch(const DwParams& p, hipStream_t s) {

@@ -585,6 +585,7 @@ class SSDLite {
     static constexpr double EPS = 1e-3;
     static constexpr int S = 320, DETS = 300, TOPK = 300;
     static constexpr double SCORE = 0.001, NMS = 0.55;
+    static constexpr int HEAD_TILE = 31;  // one x6b tile for the grouped head 1x1 convs (64 x 128)
 
     SSDLite(const Config& c, Packer& pk) : cfg_(c), pk_(pk), blocks_(mnv3_blocks(c.reduced_tail)) {}
 
@@ -825,37 +826,62 @@ class SSDLite {
             sh.cls = P.buf({Btot, A, NC}, 4, "cls_logits");
             sh.reg = P.buf({Btot, A, 4}, 4, "bbox_regression");
         }
+        // SSDLiteHead: per map a depthwise 3x3 (+BN, ReLU6) then a 1x1 conv with bias, for the cls and
+        // the reg branch.  The weights are packed in the module order (map, branch); the records run as
+        // two grouped launches (EDGEDET_OP_GROUP): the twelve depthwise convs, then the twelve 1x1
+        // convs, which store straight into the concatenated head tensors (pixel stride 6 * cols, map
+        // anchor offset) -- 24 sequential launches per chain become 2.
+        struct HeadOp {
+            std::string p;
+            int64_t cols, off;
+            int out;
+            const Cur* f;
+        };
+        std::vector<HeadOp> hops;
         int64_t off = 0;
-        if (nch == 1) P.fork(3);
-        int br = 0;
         for (size_t i = 0; i < feats.size(); ++i) {
             const Cur& f = feats[i];
             for (int h = 0; h < 2; ++h) {
                 const std::string name = h == 0 ? "classification_head" : "regression_head";
                 const int64_t cols = h == 0 ? NC : 4;
-                const int out = h == 0 ? sh.cls : sh.reg;
                 const std::string p = "head." + name + ".module_list." + std::to_string(i);
-                if (nch == 1) P.lane(br % 4);
-                ++br;
-                DwOut t = dw(f, p + ".0", 3, 1, A_R6, false);
-                ConvW w = pk_.conv_bias(p + ".1.weight", p + ".1.bias", 6 * cols, f.s[3], 1);
-                ConvArgs a;
-                a.x = t.y.x;
-                a.xs = t.y.s;
-                a.w = w;
-                a.cout = 6 * cols;
-                a.k = 1;
-                a.y = P.ref(out);
-                a.ys = {B, f.s[1], f.s[2], 6 * cols};
-                a.y_pstride = 6 * cols;
-                a.y_bstride = A * cols;
-                a.y_off = (int64_t)img0 * A * cols + off * cols;
-                a.name = p + ".1" + sfx;
-                conv_op(P, a);
+                cbn(p + ".0", f.s[3], f.s[3], 3, true);  // pack order: module order
+                pk_.conv_bias(p + ".1.weight", p + ".1.bias", 6 * cols, f.s[3], 1);
+                hops.push_back({p, cols, off, h == 0 ? sh.cls : sh.reg, &f});
             }
             off += f.s[1] * f.s[2] * 6;
         }
-        if (nch == 1) P.join();
+        const int ng = (int)hops.size();
+        auto group = [&](const std::string& name) {
+            OpRec g;
+            g.kind = EDGEDET_OP_GROUP;
+            g.name = name + sfx;
+            g.i[0] = ng;
+            P.add(g);
+        };
+        std::vector<Cur> hdw;
+        group("head.depthwise");
+        for (auto& h : hops) hdw.push_back(dw(*h.f, h.p + ".0", 3, 1, A_R6, false).y);
+        group("head.pointwise");
+        for (int k = 0; k < ng; ++k) {
+            const HeadOp& h = hops[(size_t)k];
+            const Cur& f = *h.f;
+            ConvW w = pk_.conv_bias(h.p + ".1.weight", h.p + ".1.bias", 6 * h.cols, f.s[3], 1);
+            ConvArgs a;
+            a.x = hdw[(size_t)k].x;
+            a.xs = hdw[(size_t)k].s;
+            a.w = w;
+            a.cout = 6 * h.cols;
+            a.k = 1;
+            a.y = P.ref(h.out);
+            a.ys = {B, f.s[1], f.s[2], 6 * h.cols};
+            a.y_pstride = 6 * h.cols;
+            a.y_bstride = A * h.cols;
+            a.y_off = (int64_t)img0 * A * h.cols + h.off * h.cols;
+            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") ? 0 : HEAD_TILE;  // f32: the members run alone
+            a.name = h.p + ".1" + sfx;
+            conv_op(P, a);
+        }
         if (pack_only) return;
 
         if (sh.anchors < 0) {

@@ -25,6 +25,8 @@ GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 SSD_STEM = 21
 MBCONV = 22
 WAIT = 23
+GROUP = 25  # the next i[0] records (CONV or DWCONV) issued as one grouped launch
+MAX_GROUP = 12
 LANE_FIELD, MAX_LANES = 47, 4
 
 SE_PARTS = 16  # max pixel splits of the SE squeeze partial sums (csrc/kernels.hpp SE_PARTS)

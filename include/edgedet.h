@@ -69,8 +69,11 @@ enum {
     EDGEDET_OP_RETINA_CLASS_NMS = 20,/* RetinaNet per (image, class): NMS over the level candidates  */
     EDGEDET_OP_SSD_STEM = 21,     /* SSDLite features.0.0 + features.0.1 in one pass                  */
     EDGEDET_OP_MBCONV = 22,       /* InvertedResidual without SE: expand, depthwise, project, residual */
-    EDGEDET_OP_WAIT = 23          /* lane i[0] waits for everything issued so far on lane i[1]         */
+    EDGEDET_OP_WAIT = 23,         /* lane i[0] waits for everything issued so far on lane i[1]         */
     /* 24 is retired (round 3's grouped SSD head kernel, measured slower and removed) */
+    EDGEDET_OP_GROUP = 25         /* the next i[0] records (all CONV or all DWCONV, same lane) issued as ONE
+                                   * grouped kernel launch; each member stays a complete record (and is
+                                   * issued alone when the members cannot share a kernel variant) */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,
@@ -78,6 +81,8 @@ enum {
  * the fork/join as graph dependencies). */
 #define EDGEDET_OP_LANE 47
 #define EDGEDET_MAX_LANES 4
+/* members of one EDGEDET_OP_GROUP launch */
+#define EDGEDET_MAX_GROUP 12
 
 /* Run ops[0..n) on `stream`.  Shapes are checked on the host before any launch; the lane topology
  * (FORK / JOIN / WAIT and every record's lane) is checked before anything is issued. */

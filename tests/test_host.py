@@ -146,11 +146,17 @@ def test_ssd_plan_lowering():
     assert ops.PREPROCESS not in kinds and ops.SSD_STEM in kinds and kinds[-1] == ops.SSD_POSTPROCESS
     stem = P.ops[kinds.index(ops.SSD_STEM)]
     assert [stem.i[k] for k in (1, 2, 7, 8)] == [320, 320, 640, 480] and P.resized == (320, 320, 320, 320)
-    assert kinds.count(ops.FORK) == kinds.count(ops.JOIN) == 1
+    # one chain at B = 4: no side lanes (the head branches are grouped launches, not lanes)
+    assert kinds.count(ops.FORK) == kinds.count(ops.JOIN) == 0
     pp = P.ops[-1]
     assert [pp.i[k] for k in range(5)] == [4, 3234, 91, 300, 300]
-    lanes = {op.lane for op in P.ops}
-    assert lanes == {0, 1, 2, 3}
+    assert {op.lane for op in P.ops} == {0}
+    # the heads: two GROUP records, the twelve depthwise convs then the twelve 1x1 convs
+    g = [k for k, kd in enumerate(kinds) if kd == ops.GROUP]
+    assert len(g) == 2 and [P.ops[k].i[0] for k in g] == [12, 12]
+    assert kinds[g[0] + 1:g[0] + 13] == [ops.DWCONV] * 12 and kinds[g[1] + 1:g[1] + 13] == [ops.CONV] * 12
+    assert [P.ops[k].name for k in range(g[1] + 1, g[1] + 13)][:2] == [
+        "head.classification_head.module_list.0.1", "head.regression_head.module_list.0.1"]
     # convs: stem 1 + blocks 0-11 (block 0 has no expansion: 1 + 11*2) + C4 split 2 + blocks 13-14 (2*2)
     #        + last 1 + extras 4*2 + head 6*2
     n_conv = kinds.count(ops.CONV)

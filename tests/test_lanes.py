@@ -30,6 +30,8 @@ GOOD = [
      (ops.JOIN, 3, 0, 0)],                                             # chain lane 1 -> 2 -> 3
     [(ops.FORK, 2, 0, 0), (ops.WAIT, 0, 2, 0), (ops.WAIT, 1, 0, 0), (ops.JOIN, 2, 0, 0)],  # lane 0 both ways
     [(M, 0, 0, 0)],
+    [(ops.GROUP, 2, 0, 0), (ops.CONV, 0, 0, 0), (ops.CONV, 0, 0, 0), (M, 0, 0, 0)],          # grouped launch
+    [(ops.FORK, 1, 0, 0), (ops.GROUP, 1, 0, 1), (ops.DWCONV, 0, 0, 1), (ops.JOIN, 1, 0, 0)],  # on a side lane
 ]
 BAD = {
     "op on a lane that is not forked": [(M, 0, 0, 1)],
@@ -39,6 +41,11 @@ BAD = {
     "join: the forked side lanes": [(ops.FORK, 2, 0, 0), (ops.JOIN, 1, 0, 0)],
     "missing JOIN": [(ops.FORK, 2, 0, 0), (M, 0, 0, 2)],
     "fork: 1..3 side lanes": [(ops.FORK, 4, 0, 0), (ops.JOIN, 4, 0, 0)],
+    "group: 1..12 following records": [(ops.GROUP, 3, 0, 0), (ops.CONV, 0, 0, 0), (ops.CONV, 0, 0, 0)],
+    "group: 1..12 following records ": [(ops.GROUP, 13, 0, 0)] + [(ops.CONV, 0, 0, 0)] * 13,
+    "group: CONV or DWCONV members": [(ops.GROUP, 1, 0, 0), (M, 0, 0, 0)],
+    "group: members of one kind on the group's lane": [(ops.GROUP, 2, 0, 0), (ops.CONV, 0, 0, 0), (ops.DWCONV, 0, 0, 0)],
+    "group on a lane that is not forked": [(ops.GROUP, 1, 0, 2), (ops.CONV, 0, 0, 2)],
 }
 
 
