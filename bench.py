@@ -287,68 +287,101 @@ def op_work(op):
     return f"kind{k}", 0.0, 0.0
 
 
+def group_members(plan, k):
+    """Indices of the records a GROUP record at k issues as one launch."""
+    return list(range(k + 1, k + 1 + int(plan.ops[k].i[0])))
+
+
 def per_op_times(plan, stream, reps=20):
-    """Average device time of each op of the plan, run alone between HIP events on `stream`."""
+    """Average device time of each launch of the plan, run alone between HIP events on `stream`: an
+    op per record, a GROUP record with its members as the one grouped launch they are (the time is
+    attributed to the GROUP record, its members get 0)."""
     import ctypes
     from edgeml_amd import ops as O
     L = O.lib()
-    res = []
-    recs = plan.records
+    recs = plan.records.copy()
+    recs["i"][:, O.LANE_FIELD] = 0  # time every launch alone on the timed stream
     sh = O.stream_handle(stream)
-    recs = recs.copy()
-    recs["i"][:, O.LANE_FIELD] = 0  # time every op alone on the timed stream
+    res = [0.0] * len(recs)
+    k = 0
     with torch.cuda.stream(stream):
-        for k in range(len(recs)):
-            if recs[k]["kind"] in (O.FORK, O.JOIN, O.WAIT, O.GROUP):
-                res.append(0.0)  # a GROUP's members are timed one by one (each alone)
+        while k < len(recs):
+            kind = recs[k]["kind"]
+            if kind in (O.FORK, O.JOIN, O.WAIT):
+                k += 1
                 continue
-            ptr = recs[k:k + 1].ctypes.data_as(ctypes.c_void_p)
-            O.check(L.edgedet_plan_run(ptr, 1, sh))
+            n = 1 + (int(recs[k]["i"][0]) if kind == O.GROUP else 0)
+            ptr = recs[k:k + n].ctypes.data_as(ctypes.c_void_p)
+            O.check(L.edgedet_plan_run(ptr, n, sh))
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(reps):
-                L.edgedet_plan_run(ptr, 1, sh)
+                L.edgedet_plan_run(ptr, n, sh)
             e1.record(stream)
             e1.synchronize()
-            res.append(e0.elapsed_time(e1) / reps)
+            res[k] = e0.elapsed_time(e1) / reps
+            k += n
     return res
 
 
 OP_DUMP = {}
 
 
+def unit_work(plan, k):
+    """(family, flops, bytes) of the launch at record k: one op, or a GROUP's members summed."""
+    from edgeml_amd import ops as O
+    op = plan.ops[k]
+    if op.kind != O.GROUP:
+        return op_work(op)
+    ws = [op_work(plan.ops[j]) for j in group_members(plan, k)]
+    return ws[0][0], sum(w[1] for w in ws), sum(w[2] for w in ws)
+
+
 def roofline_for(plan, stream, step_ms, model=""):
     """Dominant kernel family of the step (by measured device time) and its longest launch, priced
-    against the roof that binds it (max of flops / fp32-MFMA peak and bytes / HBM peak)."""
-    times = per_op_times(plan, stream)
+    against the roof that binds it (max of flops / the MFMA peak and bytes / HBM peak).  A grouped
+    launch (EDGEDET_OP_GROUP) is one launch: its members' work summed, its kernel the grouped one."""
     from edgeml_amd import ops as O
-    OP_DUMP[model] = [{"name": op.name, "family": op_work(op)[0], "ms": round(t, 5), "flops": op_work(op)[1],
-                       "bytes": op_work(op)[2],
+    times = per_op_times(plan, stream)
+    in_group = set()
+    for k, op in enumerate(plan.ops):
+        if op.kind == O.GROUP:
+            in_group.update(group_members(plan, k))
+    units = [k for k, op in enumerate(plan.ops) if k not in in_group and op.kind not in (O.FORK, O.JOIN, O.WAIT)]
+    OP_DUMP[model] = [{"name": op.name, "family": op_work(op)[0] if op.kind != O.GROUP else "group",
+                       "ms": round(t, 5), "flops": op_work(op)[1], "bytes": op_work(op)[2],
+                       "in_group": k in in_group,
                        "tile": conv_tile(plan.records[k:k + 1]) if op.kind == O.CONV else None}
                       for k, (op, t) in enumerate(zip(plan.ops, times))]
     fam = {}
-    for op, t in zip(plan.ops, times):
-        name = op_work(op)[0]
-        if name != "lanes":
-            fam[name] = fam.get(name, 0.0) + t
+    for k in units:
+        name = unit_work(plan, k)[0]
+        fam[name] = fam.get(name, 0.0) + times[k]
     dom = max(fam, key=fam.get)
     # the family's largest launch by algorithmic work (first in plan order among equal shapes, so
     # the choice does not flip between identical layers from run to run and the committed PMC
     # summary of the same launch applies); its measured time prices it
-    op, t = max(((o, t) for o, t in zip(plan.ops, times) if op_work(o)[0] == dom),
-                key=lambda x: (op_work(x[0])[1], op_work(x[0])[2]))
-    name, flops, byts = op_work(op)
+    k = max((j for j in units if unit_work(plan, j)[0] == dom), key=lambda j: (unit_work(plan, j)[1], unit_work(plan, j)[2]))
+    op, t = plan.ops[k], times[k]
+    name, flops, byts = unit_work(plan, k)
     kname, peak_tf = {"dwconv": "dwconv_kernel"}.get(name, name), FP32_MFMA_PEAK_TFS
-    k = plan.ops.index(op)
+    grouped = op.kind == O.GROUP
     if name == "conv":
-        kname, wg, nt, peak_tf = conv_grid(op, plan.records[k:k + 1])
+        if grouped:
+            wg, peak_tf = 0, FP32_MFMA_PEAK_TFS
+            for j in group_members(plan, k):
+                kn, w_, nt, peak_tf = conv_grid(plan.ops[j], plan.records[j:j + 1])
+                wg += w_
+            kname = kn.replace("conv_x6b_kernel", "conv_x6b_group_kernel")
+        else:
+            kname, wg, nt, peak_tf = conv_grid(op, plan.records[k:k + 1])
     t_f = flops / (peak_tf * 1e12)
     t_b = byts / (HBM_PEAK_GBS * 1e9)
-    out = {"kernel": kname, "launch": op.name,
+    out = {"kernel": kname, "launch": op.name, "members": len(group_members(plan, k)) if grouped else 1,
            "launch_ms": round(t, 4), "algorithmic_flops": flops, "algorithmic_bytes": byts,
-           "family_ms": {k: round(v, 4) for k, v in sorted(fam.items(), key=lambda kv: -kv[1])},
-           "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3)}
+           "family_ms": {f: round(v, 4) for f, v in sorted(fam.items(), key=lambda kv: -kv[1])},
+           "sum_ops_ms": round(sum(times), 3), "step_ms": round(step_ms, 3), "launches": launch_count(plan)}
     if name == "conv":
         out["grid_wg"], out["wg_threads"] = wg, nt
         if kname.startswith("conv_x6"):
@@ -362,15 +395,39 @@ def roofline_for(plan, stream, step_ms, model=""):
         out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4)})
     out["traffic"] = None
-    out["_op_index"] = plan.ops.index(op)
     return out
+
+
+def launch_count(plan):
+    """Kernel launches per forward: every record but FORK / JOIN / WAIT, a GROUP's members as one
+    (records that issue two kernels -- the SSD post-process (class selection + image NMS), an SE
+    excitation wider than the fused kernel takes, a pre-split conv -- counted as two)."""
+    from edgeml_amd import ops as O
+    n, k = 0, 0
+    while k < len(plan.ops):
+        op = plan.ops[k]
+        if op.kind == O.GROUP:
+            n += 1
+            k += 1 + int(op.i[0])
+            continue
+        if op.kind in (O.FORK, O.JOIN, O.WAIT):
+            pass
+        elif op.kind == O.SSD_POSTPROCESS:
+            n += 2
+        elif op.kind == O.SE_FC:
+            n += 1 if op.i[1] * op.i[2] <= 8192 else 2
+        elif op.kind == O.CONV and op.p.get(8) is not None and conv_tile(plan.records[k:k + 1]) == 25:
+            n += 2
+        else:
+            n += 1
+        k += 1
+    return {"records": len(plan.ops), "kernel_launches": n}
 
 
 def attach_traffic(roof, model):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_<model>.json, produced by tools/pmc_summary.py from separate FETCH_SIZE and
     WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction applied there); None if absent or stale."""
-    roof.pop("_op_index", None)
     path = os.path.join(ROOT, "profiles", f"pmc_{model}.json")
     try:
         with open(path) as f:
