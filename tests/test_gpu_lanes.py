@@ -64,3 +64,39 @@ def test_side_lane_wait_chain_direct_and_captured():
         s.synchronize()
         assert torch.equal(out.tensor().cpu(), out_seq.tensor().cpu())
     assert ops.lib().edgedet_lane_sets() >= 1
+
+
+def test_lane_set_takeover_keeps_older_graphs_valid():
+    """The LRU takeover of csrc/exec.hip lanes_for: at most 16 lane sets per device, a caller stream
+    beyond that takes over the least recently used set (re-keyed, never destroyed).  Capture the side
+    lane chain on 33 distinct caller streams (so every earlier stream's set has been taken over at
+    least once, whatever sets other tests left), then replay the OLDEST graph on its own stream and the
+    newest on its stream, interleaved: both give the sequential result."""
+    import ctypes
+    seq, out_seq, _ = _build(False)
+    seq.run()
+    torch.cuda.synchronize()
+    want = out_seq.tensor().cpu()
+    P, out, _ = _build(True)
+    L = ops.lib()
+    streams, graphs = [], []
+    try:
+        for k in range(33):
+            s = torch.cuda.Stream()
+            g = ctypes.c_void_p()
+            ops.check(L.edgedet_graph_create(P.records.ctypes.data_as(ctypes.c_void_p), len(P.records),
+                                             ops.stream_handle(s), ctypes.byref(g)))
+            streams.append(s)
+            graphs.append(g)
+        assert L.edgedet_lane_sets() <= 16
+        for r in range(3):
+            for k in (0, 32, 16):
+                out.tensor().zero_()
+                torch.cuda.synchronize()
+                ops.check(L.edgedet_graph_launch(graphs[k], ops.stream_handle(streams[k])))
+                streams[k].synchronize()
+                assert torch.equal(out.tensor().cpu(), want), (r, k)
+    finally:
+        torch.cuda.synchronize()
+        for g in graphs:
+            L.edgedet_graph_destroy(g)

@@ -31,5 +31,9 @@ for c in ${CHAINS:-}; do
     EDGEDET_SSD_CHAINS=$c step chains${c}_if${inf} 300 python -u bench.py --model ssd --steps 400 --warmup 20 --no-cpu --no-e2e --no-roofline --no-alt --inflight $inf
   done
 done
+if [ "${LANE_REPRO:-0}" = "1" ]; then  # one variant per process; stop at the first that dies
+  [ -x tools/lane_repro ] || hipcc -O2 --offload-arch=gfx950 tools/lane_repro.cpp -o tools/lane_repro || exit 8
+  for m in none events streams both; do step lane_repro_$m 60 tools/lane_repro $m; done
+fi
 if [ -n "${EXTRA:-}" ]; then step extra 900 bash -c "$EXTRA"; fi
 exit 0
