@@ -1069,6 +1069,7 @@ class ResNetFPN {
         bool in_relu = false;
         int out = -1;  // store into this buffer (pixel stride out_p, batch stride out_b, element offset out_off)
         int64_t out_p = -1, out_b = -1, out_off = 0;
+        int tile = 0;  // 0 = the tuned table's
     };
 
     Cur conv(Plan& P, const Cur& in, const std::string& wkey, int64_t cout, int k, int stride, int act,
@@ -1102,6 +1103,7 @@ class ResNetFPN {
         a.in_scale = o.in_scale;
         a.in_shift = o.in_shift;
         a.name = o.name.empty() ? wkey : o.name;
+        a.tile = o.tile;
         if (o.out >= 0) {
             a.y_pstride = o.out_p;
             a.y_bstride = o.out_b;
@@ -1241,6 +1243,7 @@ static std::vector<float> grid_anchors(int gh, int gw, int Hp, int Wp, const std
 class FasterRCNN : public ResNetFPN {
   public:
     static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
+    static constexpr int RPN_TILE = 25;  // the grouped RPN 3x3 convs: the P2 level's tuned tile (256 x 128)
     static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
                             BOX_MIN = 1e-2;
 
@@ -1286,16 +1289,43 @@ class FasterRCNN : public ResNetFPN {
         const int Aa = 3;
         std::vector<std::pair<Ref, Ref>> heads;
         std::vector<std::pair<int, int>> grids;
-        // the five levels in order on the caller stream (on four stream lanes measured 0.75 % slower at
-        // two plans in flight: eight streams over four hardware queues, round 3)
-        for (size_t lvl = 0; lvl < outs.size(); ++lvl) {
+        // The shared 3x3 convs of the five levels as two grouped launches (EDGEDET_OP_GROUP): each 3x3
+        // conv of every level in one launch on the P2 level's tile, so the small levels' workgroups fill
+        // the big level's tail instead of running as eight latency-bound launches after it (round 3 ran
+        // the levels one after another on the caller stream; on four stream lanes was 0.75 % slower).
+        const int L5 = (int)outs.size();
+        auto rpn_group = [&](const std::string& name) {
+            OpRec g;
+            g.kind = EDGEDET_OP_GROUP;
+            g.name = name;
+            g.i[0] = L5;
+            P.add(g);
+        };
+        const bool grouped = !env_is("EDGEDET_CONV_MATH", "f32", "bf16x6");  // grouped launches: bf16x6 tiles
+        std::vector<Cur> t0s, t1s;
+        if (grouped) rpn_group("rpn.head.conv.0");
+        for (int lvl = 0; lvl < L5; ++lvl) {
+            COpt o;
+            o.bias_key = "rpn.head.conv.0.0.bias";
+            o.name = "rpn.head.conv.0@" + std::to_string(lvl);
+            o.tile = grouped ? RPN_TILE : 0;
+            t0s.push_back(conv(P, outs[(size_t)lvl], "rpn.head.conv.0.0.weight", 256, 3, 1, A_RE, o));
+        }
+        if (grouped) rpn_group("rpn.head.conv.1");
+        for (int lvl = 0; lvl < L5; ++lvl) {
+            COpt o;
+            o.bias_key = "rpn.head.conv.1.0.bias";
+            o.name = "rpn.head.conv.1@" + std::to_string(lvl);
+            o.tile = grouped ? RPN_TILE : 0;
+            t1s.push_back(conv(P, t0s[(size_t)lvl], "rpn.head.conv.1.0.weight", 256, 3, 1, A_RE, o));
+        }
+        for (int lvl = 0; lvl < L5; ++lvl) {
             const std::string at = "@" + std::to_string(lvl);
-            Cur t = conv_b(P, outs[lvl], "rpn.head.conv.0.0", 256, 3, 1, A_RE, "rpn.head.conv.0" + at);
-            t = conv_b(P, t, "rpn.head.conv.1.0", 256, 3, 1, A_RE, "rpn.head.conv.1" + at);
+            const Cur& t = t1s[(size_t)lvl];
             Cur o = conv_b(P, t, "rpn.head.cls_logits", 3, 1, 1, A_NONE, "rpn.head.cls_logits" + at);
             Cur d = conv_b(P, t, "rpn.head.bbox_pred", 12, 1, 1, A_NONE, "rpn.head.bbox_pred" + at);
             heads.push_back({o.x, d.x});
-            grids.push_back({(int)outs[lvl].s[1], (int)outs[lvl].s[2]});
+            grids.push_back({(int)outs[(size_t)lvl].s[1], (int)outs[(size_t)lvl].s[2]});
         }
         std::vector<int> anchor_bufs;
         const int sizes[5] = {32, 64, 128, 256, 512};
