@@ -427,6 +427,9 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
         written += tot_eq;
     } else if (need_eq > 0) {
         int eq_taken = 0;
+        // unrolled (kr stays in registers: a runtime index into it would move the whole array to
+        // scratch); the break is uniform (eq_taken is a block total)
+#pragma unroll
         for (int j = 0; j < PER; ++j) {
             const bool eq = kr[j] == T;
             int tj;
