@@ -408,8 +408,9 @@ def roofline_for(plan, stream, step_ms, model=""):
 
 def launch_count(plan):
     """Kernel launches per forward: every record but FORK / JOIN / WAIT, a GROUP's members as one
-    (records that issue two kernels -- the SSD post-process (class selection + image NMS), an SE
-    excitation wider than the fused kernel takes, a pre-split conv -- counted as two)."""
+    (records that issue two kernels -- the SSD post-process (class selection + image NMS), the
+    chunked RPN filter, an SE excitation wider than the fused kernel takes, a pre-split conv -- counted
+    as two)."""
     from edgeml_amd import ops as O
     n, k = 0, 0
     while k < len(plan.ops):
@@ -422,6 +423,8 @@ def launch_count(plan):
             pass
         elif op.kind == O.SSD_POSTPROCESS:
             n += 2
+        elif op.kind == O.RPN_LEVEL_NMS:
+            n += 2 if op.p.get(20) is not None else 1  # chunked top-k: chunk select + level kernel
         elif op.kind == O.SE_FC:
             n += 1 if op.i[1] * op.i[2] <= 8192 else 2
         elif op.kind == O.CONV and op.p.get(8) is not None and conv_tile(plan.records[k:k + 1]) == 25:

@@ -1143,6 +1143,40 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 
 // ================================================================ RPN per-level selection
 
+// rpn_chunk_select_kernel: one workgroup per (chunk of P.chunk anchors, level, image) keeps the
+// chunk's top-k logits (ties in index order) unsorted, in index order, with their level indices.  Every
+// element of a level's top-k is in its chunk's top-k, so the union of the chunk lists, chunks in order,
+// holds the level's top-k with the index order preserved: the level kernel then selects from at most
+// nchunk x KC entries instead of streaming the whole level (120,000 logits per image at P2) through its
+// five radix passes.
+template <int NT, int KC>
+__global__ void __launch_bounds__(NT) rpn_chunk_select_kernel(RpnParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
+    const int c = blockIdx.x, l = blockIdx.y, b = blockIdx.z;
+    const RpnLevel L = P.lv[l];
+    const int64_t slot = ((int64_t)(b * P.nlevels + l) * P.nchunk + c);
+    const int start = c * P.chunk;
+    if (start >= L.n) {
+        if (threadIdx.x == 0) P.ccount[slot] = 0;
+        return;
+    }
+    const int nc = min(P.chunk, L.n - start);
+    const float* ob = L.obj + (int64_t)b * L.n + start;
+    auto fkey = [&](int i, uint32_t& k) -> bool {
+        k = float_key(ob[i]);
+        return true;
+    };
+    const uint32_t T = radix_select<NT>(nc, P.topk, fkey, S.hist, S.misc);
+    const bool take_all = S.misc[1] <= P.topk;
+    const int m = compact<NT>(nc, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    for (int t = threadIdx.x; t < m; t += NT) {
+        P.ckey[slot * KC + t] = (uint32_t)(S.keys[t] >> 32);
+        P.cidx[slot * KC + t] = start + key_index(S.keys[t]);
+    }
+    if (threadIdx.x == 0) P.ccount[slot] = m;
+}
+
 template <int NT, int KC>
 __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1151,25 +1185,38 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
     const RpnLevel L = P.lv[l];
     const float* ob = L.obj + (int64_t)b * L.n;
     const f32x4* db = reinterpret_cast<const f32x4*>(L.deltas) + (int64_t)b * L.n;
+    // candidates: the whole level, or the union of its chunk lists (position i -> level index cidx[i])
+    const bool chunked = P.ckey != nullptr;
+    const int64_t cbase = (int64_t)(b * P.nlevels + l) * P.nchunk;
+    const uint32_t* ck = chunked ? P.ckey + cbase * KC : nullptr;
+    const int* ci = chunked ? P.cidx + cbase * KC : nullptr;
+    const int* cc = chunked ? P.ccount + cbase : nullptr;
+    const int n = chunked ? (L.n + P.chunk - 1) / P.chunk * KC : L.n;
     auto fkey = [&](int i, uint32_t& k) -> bool {
-        k = float_key(ob[i]);
-        return true;
+        if (!chunked) {
+            k = float_key(ob[i]);
+            return true;
+        }
+        const int ch = i / KC, r = i - ch * KC;
+        k = ck[i];
+        return r < cc[ch];
     };
+    auto level_index = [&](int i) { return chunked ? ci[i] : i; };
 #ifdef RPN_PROFILE
     long long tp = __builtin_amdgcn_s_memtime(), t_sel = 0, t_cmp = 0, t_sort = 0, t_dec = 0, t_nms = 0;
 #define RPN_STAMP(acc) do { __syncthreads(); const long long tn = __builtin_amdgcn_s_memtime(); acc += tn - tp; tp = tn; } while (0)
 #else
 #define RPN_STAMP(acc) do { } while (0)
 #endif
-    const uint32_t T = radix_select<NT>(L.n, P.topk, fkey, S.hist, S.misc);
+    const uint32_t T = radix_select<NT>(n, P.topk, fkey, S.hist, S.misc);
     RPN_STAMP(t_sel);
     const bool take_all = S.misc[1] <= P.topk;
-    const int m = compact<NT>(L.n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    const int m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
     RPN_STAMP(t_cmp);
     bitonic_desc<NT>(S.keys, nullptr, m);
     RPN_STAMP(t_sort);
     for (int t = threadIdx.x; t < m; t += NT) {
-        const int i = key_index(S.keys[t]);
+        const int i = level_index(key_index(S.keys[t]));
         const f32x4 d = db[i];
         const f32x4 an = *reinterpret_cast<const f32x4*>(L.anchors + (int64_t)i * 4);
         const f32x4 bx = clip_box(decode_box(d, an, 1.f, 1.f, 1.f, 1.f), P.img_h, P.img_w);
@@ -1611,6 +1658,15 @@ int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s) {
     for (int l = 0; l < P.nlevels; ++l)
         EDGEDET_REQUIRE(P.lv[l].obj && P.lv[l].deltas && P.lv[l].anchors && P.lv[l].n > 0, "rpn: null/empty level");
     constexpr int KC = 1024, NT = 512;
+    if (P.ckey) {
+        EDGEDET_REQUIRE(P.cidx && P.ccount && P.chunk >= P.topk && P.nchunk >= 1, "rpn: chunk scratch");
+        for (int l = 0; l < P.nlevels; ++l)
+            EDGEDET_REQUIRE((P.lv[l].n + P.chunk - 1) / P.chunk <= P.nchunk, "rpn: a level exceeds nchunk chunks");
+        auto k1 = rpn_chunk_select_kernel<NT, KC>;
+        if (set_lds(k1, seg_smem<KC>())) return -2;
+        hipLaunchKernelGGL(k1, dim3(P.nchunk, P.nlevels, P.B), dim3(NT), seg_smem<KC>(), s, P);
+        EDGEDET_LAUNCH_CHECK();
+    }
     auto k = rpn_level_nms_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;
     hipLaunchKernelGGL(k, dim3(P.nlevels, P.B), dim3(NT), seg_smem<KC>(), s, P, out);

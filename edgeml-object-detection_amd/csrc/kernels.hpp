@@ -155,6 +155,13 @@ struct RpnParams {
     int nlevels, ld, A, B, topk;
     float img_h, img_w, min_size, score_thresh;
     IouThr iou;
+    // chunked top-k (optional, ckey != null): a first launch keeps each chunk's top-k of every
+    // (image, level) in ckey / cidx [B][nlevels][nchunk][KC] (counts in ccount), and the level kernel
+    // selects from the union of its chunks instead of streaming the whole level five times
+    uint32_t* ckey;
+    int* cidx;
+    int* ccount;
+    int chunk, nchunk;
 };
 
 struct MergeParams {

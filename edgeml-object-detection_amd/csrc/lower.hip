@@ -1243,7 +1243,8 @@ static std::vector<float> grid_anchors(int gh, int gw, int Hp, int Wp, const std
 class FasterRCNN : public ResNetFPN {
   public:
     static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
-    static constexpr int RPN_TILE = 25;  // the grouped RPN 3x3 convs: the P2 level's tuned tile (256 x 128)
+    static constexpr int RPN_TILE = 25;
+    static constexpr int RPN_CHUNK = 8192;  // anchors per chunk of the chunked RPN top-k  // the grouped RPN 3x3 convs: the P2 level's tuned tile (256 x 128)
     static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
                             BOX_MIN = 1e-2;
 
@@ -1357,6 +1358,15 @@ class FasterRCNN : public ResNetFPN {
             o.f[2] = (float)RPN_MIN;
             o.f[3] = (float)RPN_SCORE;
             o.d[0] = RPN_NMS;
+            // chunked top-k: 8,192 anchors per chunk (P2 of an 800 x 800 image: 15 chunks per image)
+            int64_t nmax = 0;
+            for (int l = 0; l < L; ++l) nmax = std::max<int64_t>(nmax, o.i[6 + l]);
+            const int64_t chunk = RPN_CHUNK, nch = (nmax + chunk - 1) / chunk;
+            o.p[20] = P.ref(P.buf({B, L, nch, 1024}, I32, "rpn.chunk.key"));
+            o.p[21] = P.ref(P.buf({B, L, nch, 1024}, I32, "rpn.chunk.idx"));
+            o.p[22] = P.ref(P.buf({B, L, nch}, I32, "rpn.chunk.count"));
+            o.i[16] = chunk;
+            o.i[17] = nch;
             P.add(o);
         }
         const int R = RPN_POST;
