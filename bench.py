@@ -276,14 +276,6 @@ def op_work(op):
         return "retina_select", 0.0, 4.0 * i[0] * n * (i[3] + 4)
     if k == O.RETINA_CLASS_NMS:
         return "retina_nms", 0.0, 4.0 * i[0] * i[1] * i[2] * 7
-    if k == O.SSD_EXTRAS:  # extra blocks 1..3: block 1's input in, every block's output out, weights
-        B, nb = i[0], i[1]
-        fl, by = 0.0, 0.0
-        for e in range(nb):
-            cin, cmid, cout, ld1, ld2, H, W, Ho, Wo = (i[2 + 9 * e + j] for j in range(9))
-            fl += 2.0 * B * (H * W * cin * cmid + Ho * Wo * cmid * (9 + cout))
-            by += 4.0 * (B * Ho * Wo * cout + cmid * (ld1 + 10) + cout * (ld2 + 1)) + (4.0 * B * H * W * cin if e == 0 else 0.0)
-        return "extras", fl, by
     if k == O.MBCONV:  # expand 1x1 + depthwise KxK + project 1x1 (+ residual): block input in, output out
         B, H, W, Cin, Cexp, Cout, Ho, Wo, K = (i[j] for j in range(9))
         fl = 2.0 * B * (H * W * Cin * Cexp + Ho * Wo * Cexp * (K * K + Cout))

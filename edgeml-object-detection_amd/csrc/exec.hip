@@ -22,8 +22,6 @@
 //                  fused SE excitation (the block's SE_FC folded in): p5 fc1 w [S][C]; p6 fc1 b; p7 fc2 w^T
 //                  [S][C]; p8 fc2 b; p9 scale [B,C] | 0; p10 tickets int [B] (zero between forwards);
 //                  i11 S; i12 squeezed pixels Ho*Wo
-//   SSD_EXTRAS     SSDLite extra blocks 1..3: p0 x [B,H,W,Cin]; block e: p[1+7e..7+7e] = w1, b1, wd, bd, w2, b2, y;
-//                  i0 B; i1 blocks; block e: i[2+9e..10+9e] = Cin, Cmid, Cout, ld1, ld2, H, W, Ho, Wo
 //   MBCONV         InvertedResidual without SE in one kernel: p0 x; p1 expand w [Cexp][i12]; p2 b1;
 //                  p3 dw w [K*K][Cexp]; p4 bd; p5 project w [Cout][i13]; p6 b2; p7 y;
 //                  i0..11 B,H,W,Cin,Cexp,Cout,Ho,Wo,K,stride,pad,act; i14 residual
@@ -247,34 +245,6 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.ld2 = (int)I[13];
             p.residual = (int)I[14];
             return mbconv_launch(p, s);
-        }
-        case EDGEDET_OP_SSD_EXTRAS: {
-            ExtrasParams p{};
-            p.x = P<const float>(o, 0);
-            p.B = (int)I[0];
-            p.nblk = (int)I[1];
-            EDGEDET_REQUIRE(p.nblk >= 1 && p.nblk <= 3, "ssd_extras: 1..3 blocks");
-            for (int e = 0; e < p.nblk; ++e) {
-                auto& k = p.blk[e];
-                k.w1 = P<const float>(o, 1 + 7 * e);
-                k.b1 = P<const float>(o, 2 + 7 * e);
-                k.wd = P<const float>(o, 3 + 7 * e);
-                k.bd = P<const float>(o, 4 + 7 * e);
-                k.w2 = P<const float>(o, 5 + 7 * e);
-                k.b2 = P<const float>(o, 6 + 7 * e);
-                k.y = P<float>(o, 7 + 7 * e);
-                const int64_t* q = I + 2 + 9 * e;
-                k.cin = (int)q[0];
-                k.cmid = (int)q[1];
-                k.cout = (int)q[2];
-                k.ld1 = (int)q[3];
-                k.ld2 = (int)q[4];
-                k.H = (int)q[5];
-                k.W = (int)q[6];
-                k.Ho = (int)q[7];
-                k.Wo = (int)q[8];
-            }
-            return ssd_extras_launch(p, s);
         }
         case EDGEDET_OP_CONV: {
             if ((diag_skip_masks()[1] >> (I[23] & 63)) & 1) return 0;

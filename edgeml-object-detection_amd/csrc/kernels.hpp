@@ -90,22 +90,6 @@ struct MbParams {
 };
 int mbconv_launch(const MbParams& p, hipStream_t s);
 
-// SSDLite's extra blocks 1..3 (SSDLiteFeatureExtractorMobileNet.extra) in one
-// launch: per block 1x1 (Cin -> Cmid) + BN + ReLU6, depthwise 3x3 stride 2 + BN + ReLU6, 1x1 (Cmid ->
-// Cout) + BN + ReLU6; each block's output is a head feature map (written) and the next block's input.
-struct ExtrasParams {
-    const float* x;  // [B][H][W][Cin] extra block 1's input (extra block 0's output)
-    struct Blk {
-        const float *w1, *b1;  // [Cmid][ld1], [Cmid]
-        const float *wd, *bd;  // [9][Cmid], [Cmid]
-        const float *w2, *b2;  // [Cout][ld2], [Cout]
-        float* y;              // [B][Ho][Wo][Cout]
-        int cin, cmid, cout, ld1, ld2, H, W, Ho, Wo;
-    } blk[3];
-    int B, nblk;
-};
-int ssd_extras_launch(const ExtrasParams& p, hipStream_t s);
-
 
 struct PoolParams {
     const float* x;

@@ -911,129 +911,6 @@ int dwconv_launch(const DwParams& p, hipStream_t s) {
     return 0;
 }
 
-// ------------------------------------------------------------------------------ SSDLite extras 1..3
-// The small extra blocks (5x5 -> 3x3 -> 2x2 -> 1x1 maps) of one image per workgroup, the activations in
-// LDS from the block input to the last output: nine launches per batch chain become one.  Exact fp32
-// (fmaf chains in channel order, as the depthwise kernels).  Phases per block, a barrier between:
-//   expand   M[p][n] = relu6(sum_k X[p][k] w1[n][k] + b1[n]): thread -> output channel n (consecutive
-//            lanes, so X[p][k] is an LDS broadcast), pixels p = g, g + G, ...; weights from L2 as
-//            float4 along k;
-//   depthwise D[q][c] = relu6(sum_taps M[tap(q)][c] wd[tap][c] + bd[c]), taps in (kh, kw) order,
-//            zero padding;
-//   project  Y[q][n] = relu6(sum_c D[q][c] w2[n][c] + b2[n]), stored to the block's feature map and
-//            kept in LDS as the next block's input.
-constexpr int EXT_NT = 512;
-constexpr int EXT_XMAX = 25 * 512, EXT_MMAX = 25 * 256, EXT_DMAX = 9 * 256, EXT_YMAX = 9 * 512;
-
-__device__ __forceinline__ float relu6f(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
-
-// out[p][n] = relu6(sum_k in[p][k] w[n][k] + b[n]) for p < P, n < N (K % 4 == 0, in / out in LDS)
-__device__ __forceinline__ void ext_pointwise(const float* __restrict__ in, int P, int K, const float* __restrict__ w,
-                                              int ld, const float* __restrict__ b, int N, float* out) {
-    const int G = EXT_NT / N;  // pixel groups (N divides EXT_NT)
-    const int n = threadIdx.x % N, g = threadIdx.x / N;
-    if (g >= G) return;
-    constexpr int PMAX = 13;  // at most ceil(25 / 2) pixels per thread (N <= 256)
-    float acc[PMAX];
-#pragma unroll
-    for (int j = 0; j < PMAX; ++j) acc[j] = 0.f;
-    const float* wr = w + (int64_t)n * ld;
-    for (int k = 0; k < K; k += 4) {
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + k);
-#pragma unroll
-        for (int j = 0; j < PMAX; ++j) {
-            const int p = g + j * G;
-            if (p < P) {
-                const float* xr = in + p * K + k;
-                acc[j] = fmaf(xr[0], wv.x, acc[j]);
-                acc[j] = fmaf(xr[1], wv.y, acc[j]);
-                acc[j] = fmaf(xr[2], wv.z, acc[j]);
-                acc[j] = fmaf(xr[3], wv.w, acc[j]);
-            }
-        }
-    }
-    const float bv = b[n];
-#pragma unroll
-    for (int j = 0; j < PMAX; ++j) {
-        const int p = g + j * G;
-        if (p < P) out[p * N + n] = relu6f(acc[j] + bv);
-    }
-}
-
-__global__ void __launch_bounds__(EXT_NT) ssd_extras_kernel(ExtrasParams p) {
-    extern __shared__ __attribute__((aligned(16))) float ext_smem[];
-    float* X = ext_smem;        // block input  [P][Cin]
-    float* M = X + EXT_XMAX;    // expanded     [P][Cmid]
-    float* D = M + EXT_MMAX;    // depthwise    [Q][Cmid]
-    float* Y = D + EXT_DMAX;    // block output [Q][Cout]
-    const int b = blockIdx.x;
-    {
-        const auto& k0 = p.blk[0];
-        const int n4 = k0.H * k0.W * k0.cin / 4;
-        const f32x4* src = reinterpret_cast<const f32x4*>(p.x + (int64_t)b * k0.H * k0.W * k0.cin);
-        for (int t = threadIdx.x; t < n4; t += EXT_NT) reinterpret_cast<f32x4*>(X)[t] = src[t];
-    }
-    __syncthreads();
-    for (int e = 0; e < p.nblk; ++e) {
-        const auto& k = p.blk[e];
-        const int P = k.H * k.W, Q = k.Ho * k.Wo;
-        ext_pointwise(X, P, k.cin, k.w1, k.ld1, k.b1, k.cmid, M);
-        __syncthreads();
-        for (int t = threadIdx.x; t < Q * k.cmid; t += EXT_NT) {
-            const int q = t / k.cmid, c = t - q * k.cmid;
-            const int oh = q / k.Wo, ow = q - oh * k.Wo;
-            float a = 0.f;
-            for (int kh = 0; kh < 3; ++kh) {
-                const int ih = oh * 2 - 1 + kh;
-                if ((unsigned)ih >= (unsigned)k.H) continue;
-                for (int kw = 0; kw < 3; ++kw) {
-                    const int iw = ow * 2 - 1 + kw;
-                    if ((unsigned)iw >= (unsigned)k.W) continue;
-                    a = fmaf(M[(ih * k.W + iw) * k.cmid + c], k.wd[(kh * 3 + kw) * k.cmid + c], a);
-                }
-            }
-            D[t] = relu6f(a + k.bd[c]);
-        }
-        __syncthreads();
-        ext_pointwise(D, Q, k.cmid, k.w2, k.ld2, k.b2, k.cout, Y);
-        __syncthreads();
-        float* yb = k.y + (int64_t)b * Q * k.cout;
-        for (int t = threadIdx.x; t < Q * k.cout; t += EXT_NT) {
-            yb[t] = Y[t];
-            X[t] = Y[t];  // the next block's input
-        }
-        __syncthreads();
-    }
-}
-
-int ssd_extras_launch(const ExtrasParams& p, hipStream_t s) {
-    EDGEDET_REQUIRE(p.x && p.B >= 1 && p.nblk >= 1 && p.nblk <= 3, "ssd_extras: 1..3 blocks");
-    for (int e = 0; e < p.nblk; ++e) {
-        const auto& k = p.blk[e];
-        EDGEDET_REQUIRE(k.w1 && k.b1 && k.wd && k.bd && k.w2 && k.b2 && k.y, "ssd_extras: null pointer");
-        EDGEDET_REQUIRE(k.cin % 4 == 0 && k.cmid % 4 == 0 && k.ld1 >= k.cin && k.ld2 >= k.cmid && k.ld1 % 4 == 0 &&
-                            k.ld2 % 4 == 0, "ssd_extras: channels and weight rows multiples of 4");
-        EDGEDET_REQUIRE(EXT_NT % k.cmid == 0 && EXT_NT % k.cout == 0 && k.cmid <= 256 && k.cout <= 512,
-                        "ssd_extras: Cmid, Cout divide 512 (Cmid <= 256)");
-        EDGEDET_REQUIRE(k.H * k.W * k.cin <= EXT_XMAX && k.H * k.W * k.cmid <= EXT_MMAX &&
-                            k.Ho * k.Wo * k.cmid <= EXT_DMAX && k.Ho * k.Wo * k.cout <= EXT_YMAX &&
-                            k.Ho * k.Wo * k.cout <= EXT_XMAX,
-                        "ssd_extras: maps exceed the LDS tiles");
-        EDGEDET_REQUIRE(k.Ho == (k.H - 1) / 2 + 1 && k.Wo == (k.W - 1) / 2 + 1, "ssd_extras: 3x3 stride 2 pad 1");
-        EDGEDET_REQUIRE((k.H * k.W + EXT_NT / k.cmid - 1) / (EXT_NT / k.cmid) <= 13 &&
-                            (k.Ho * k.Wo + EXT_NT / k.cout - 1) / (EXT_NT / k.cout) <= 13,
-                        "ssd_extras: at most 13 pixels per thread");
-        if (e > 0)
-            EDGEDET_REQUIRE(k.cin == p.blk[e - 1].cout && k.H == p.blk[e - 1].Ho && k.W == p.blk[e - 1].Wo,
-                            "ssd_extras: block e's input is block e-1's output");
-    }
-    const size_t lds = sizeof(float) * (EXT_XMAX + EXT_MMAX + EXT_DMAX + EXT_YMAX);
-    if (int rc = mbw_set_lds(ssd_extras_kernel, lds)) return rc;
-    hipLaunchKernelGGL(ssd_extras_kernel, dim3((unsigned)p.B), dim3(EXT_NT), lds, s, p);
-    EDGEDET_LAUNCH_CHECK();
-    return 0;
-}
-
 // ------------------------------------------------------------------------------ SE squeeze
 // Standalone adaptive_avg_pool2d(1) for an SE whose producer is not a depthwise conv: grid
 // (cdiv(C, 64), B), block 256 = 64 channels x 4 pixel groups, fixed-order reduction.  (The SSDLite

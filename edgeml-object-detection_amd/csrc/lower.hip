@@ -808,41 +808,12 @@ class SSDLite {
         cur = conv(cur, "backbone.features.1.3", 6 * c4, 1, 1, A_HS);
         feats.push_back(cur);
         const int outs[4] = {512, 256, 256, 128};
-        // extra block 0 (10x10 -> 5x5) as three ops; blocks 1..3 (5x5 -> 1x1) as one SSD_EXTRAS record:
-        // one workgroup per image keeps their activations in LDS (nine launches per chain become one)
-        OpRec xo;
-        xo.kind = EDGEDET_OP_SSD_EXTRAS;
-        xo.name = "backbone.extra.1-3" + sfx;
         for (int e = 0; e < 4; ++e) {
             const std::string p = "backbone.extra." + std::to_string(e);
-            if (e == 0 || pack_only) {
-                cur = conv(cur, p + ".0", outs[e] / 2, 1, 1, A_R6);
-                cur = dw(cur, p + ".1", 3, 2, A_R6, false).y;
-                cur = conv(cur, p + ".2", outs[e], 1, 1, A_R6);
-                feats.push_back(cur);
-                continue;
-            }
-            const int64_t cin = cur.s[3], cmid = outs[e] / 2, cout = outs[e];
-            ConvW w1 = cbn(p + ".0", cmid, cin, 1, false);
-            ConvW wd = cbn(p + ".1", cmid, cmid, 3, true);
-            ConvW w2 = cbn(p + ".2", cout, cmid, 1, false);
-            const int64_t Ho = (cur.s[1] - 1) / 2 + 1, Wo = (cur.s[2] - 1) / 2 + 1;
-            std::vector<int64_t> ys = {B, Ho, Wo, cout};
-            const int y = P.buf(ys, 4, p + ".2" + sfx);
-            const int k = e - 1;
-            if (k == 0) xo.p[0] = cur.x;
-            const Ref ps[7] = {Plan::wref(w1.w), Plan::wref(w1.b), Plan::wref(wd.w), Plan::wref(wd.b),
-                               Plan::wref(w2.w), Plan::wref(w2.b), P.ref(y)};
-            for (int j = 0; j < 7; ++j) xo.p[1 + 7 * k + j] = ps[j];
-            const int64_t iv[9] = {cin, cmid, cout, w1.Kpad, w2.Kpad, cur.s[1], cur.s[2], Ho, Wo};
-            for (int j = 0; j < 9; ++j) xo.i[2 + 9 * k + j] = iv[j];
-            cur = Cur{P.ref(y), ys};
+            cur = conv(cur, p + ".0", outs[e] / 2, 1, 1, A_R6);
+            cur = dw(cur, p + ".1", 3, 2, A_R6, false).y;
+            cur = conv(cur, p + ".2", outs[e], 1, 1, A_R6);
             feats.push_back(cur);
-        }
-        if (!pack_only) {
-            xo.i[0] = B;
-            xo.i[1] = 3;
-            P.add(xo);
         }
         std::vector<std::pair<int, int>> grids;
         int64_t A = 0;

@@ -25,7 +25,6 @@ GN_STATS, RETINA_SELECT, RETINA_CLASS_NMS = 18, 19, 20
 SSD_STEM = 21
 MBCONV = 22
 WAIT = 23
-SSD_EXTRAS = 26  # SSDLite extra blocks 1..3 in one launch
 GROUP = 25  # the next i[0] records (CONV or DWCONV) issued as one grouped launch
 MAX_GROUP = 12
 LANE_FIELD, MAX_LANES = 47, 4

@@ -76,10 +76,9 @@ enum {
     EDGEDET_OP_MBCONV = 22,       /* InvertedResidual without SE: expand, depthwise, project, residual */
     EDGEDET_OP_WAIT = 23,         /* lane i[0] waits for everything issued so far on lane i[1]         */
     /* 24 is retired (round 3's grouped SSD head kernel, measured slower and removed) */
-    EDGEDET_OP_GROUP = 25,        /* the next i[0] records (all CONV or all DWCONV, same lane) issued as ONE
+    EDGEDET_OP_GROUP = 25         /* the next i[0] records (all CONV or all DWCONV, same lane) issued as ONE
                                    * grouped kernel launch; each member stays a complete record (and is
                                    * issued alone when the members cannot share a kernel variant) */
-    EDGEDET_OP_SSD_EXTRAS = 26    /* SSDLite extra blocks 1..3 (1x1, dw 3x3 s2, 1x1; BN, ReLU6) in one pass */
 };
 
 /* i[EDGEDET_OP_LANE] of every record selects the stream it is issued on: 0 = the caller's stream,

@@ -493,52 +493,3 @@ def test_dwconv_fused_se_excitation(B, H, W, C, S, k, s):
         err = (scale.cpu() - scale_ref).abs().max().item()
         assert err < 1e-5, err
         assert int(tickets.abs().sum().item()) == 0  # reset by every image's last workgroup
-
-
-@pytest.mark.parametrize("B,cin", [(16, 512), (3, 512)])
-def test_ssd_extras_fused_matches_torch(B, cin):
-    """SSDLite extra blocks 1..3 in one SSD_EXTRAS launch (csrc/layers.hip ssd_extras_kernel) against
-    torch fp32: per block relu6(conv1x1) -> relu6(depthwise 3x3 s2 p1) -> relu6(conv1x1), 5x5 -> 3x3 ->
-    2x2 -> 1x1; every block's output is compared (they are head feature maps)."""
-    import ctypes
-    from edgeml_amd import ops
-    from edgeml_amd.plan import pack_conv_weight, pack_dw_weight
-    g = torch.Generator().manual_seed(B)
-    x = torch.rand(B, cin, 5, 5, generator=g) * 2
-    dims = [(cin, 128, 256), (256, 128, 256), (256, 64, 128)]
-    keep, refs = [], []
-    r = np.zeros(1, dtype=ops.OP_DTYPE)
-    r[0]["kind"] = ops.SSD_EXTRAS
-    r[0]["i"][0], r[0]["i"][1] = B, 3
-    t, H = x, 5
-    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
-    r[0]["p"][0] = xd.data_ptr()
-    for e, (ci, cm, co) in enumerate(dims):
-        w1 = torch.randn(cm, ci, 1, 1, generator=g) / ci ** 0.5
-        b1 = torch.randn(cm, generator=g) * 0.1
-        wd = torch.randn(cm, 1, 3, 3, generator=g) / 3
-        bd = torch.randn(cm, generator=g) * 0.1
-        w2 = torch.randn(co, cm, 1, 1, generator=g) / cm ** 0.5
-        b2 = torch.randn(co, generator=g) * 0.1
-        t = F.relu6(F.conv2d(t, w1, b1))
-        t = F.relu6(F.conv2d(t, wd, bd, 2, 1, 1, cm))
-        t = F.relu6(F.conv2d(t, w2, b2))
-        refs.append(t)
-        Ho = (H - 1) // 2 + 1
-        p1, _, k1, _ = pack_conv_weight(w1.numpy())
-        p2, _, k2, _ = pack_conv_weight(w2.numpy())
-        y = torch.zeros(B, Ho, Ho, co, device=DEV)
-        tens = [torch.from_numpy(p1).to(DEV), b1.to(DEV), torch.from_numpy(pack_dw_weight(wd.numpy())).to(DEV),
-                bd.to(DEV), torch.from_numpy(p2).to(DEV), b2.to(DEV), y]
-        keep += tens
-        for j, tt in enumerate(tens):
-            r[0]["p"][1 + 7 * e + j] = tt.data_ptr()
-        for j, v in enumerate((ci, cm, co, k1, k2, H, H, Ho, Ho)):
-            r[0]["i"][2 + 9 * e + j] = v
-        H = Ho
-    ops.check(ops.lib().edgedet_plan_run(r.ctypes.data_as(ctypes.c_void_p), 1, ops.stream_handle()))
-    torch.cuda.synchronize()
-    for e, ref in enumerate(refs):
-        got = keep[7 * e + 6].permute(0, 3, 1, 2).cpu()
-        err = (got - ref).abs().max().item()
-        assert err < 1e-4 * max(1.0, ref.abs().max().item()), (e, err)

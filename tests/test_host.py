@@ -170,13 +170,8 @@ def test_ssd_plan_lowering():
     mb = kinds.count(ops.MBCONV)
     assert mb == (0 if os.environ.get("EDGEDET_MB_BLOCK") == "0" else 2)
     heads = 12
-    # extra blocks 1..3 as one SSD_EXTRAS record (three depthwise and six convs fewer)
-    assert kinds.count(ops.SSD_EXTRAS) == 1
-    ex = P.ops[kinds.index(ops.SSD_EXTRAS)]
-    assert ex.i[1] == 3 and [ex.i[2 + 9 * e + 2] for e in range(3)] == [256, 256, 128]
-    assert [(ex.i[2 + 9 * e + 5], ex.i[2 + 9 * e + 7]) for e in range(3)] == [(5, 3), (3, 2), (2, 1)]
-    assert n_dw == 15 + 4 - 3 + heads - stem - mb
-    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 - 6 + heads - 2 * stem - 2 * mb
+    assert n_dw == 15 + 4 + heads - stem - mb
+    assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + heads - 2 * stem - 2 * mb
     # the SE excitations run inside their depthwise launches (fused squeeze + excitation): no SE_FC
     assert kinds.count(ops.SE_FC) == 0
     se = [op for op in P.ops if op.kind == ops.DWCONV and op.p.get(9) is not None]
