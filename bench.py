@@ -440,8 +440,7 @@ def attach_traffic(roof, model):
     # "#k" names the k-th batch chain's copy of a layer: the chains split the batch evenly, so
     # every copy has the same shape and grid and one PMC summary covers them all
     same = lambda a: (a or "").split("#")[0]
-    kernel_ok = not (pmc.get("kernel") and roof.get("kernel")) or pmc["kernel"] == roof["kernel"]
-    if same(pmc.get("launch")) == same(roof.get("launch")) and pmc.get("grid_wg") == roof.get("grid_wg") and kernel_ok:
+    if same(pmc.get("launch")) == same(roof.get("launch")) and pmc.get("grid_wg") == roof.get("grid_wg"):
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["traffic_source"] = os.path.relpath(path, ROOT)
 

@@ -18,10 +18,7 @@
 //   SSD_STEM       p0 x NHWC4; p1 w0 [16][i5]; p2 b0; p3 wd [9][16]; p4 bd; p5 w1 [16][i6]; p6 b1; p7 y;
 //                  i0..4 B,H,W,Ho,Wo (SSDLite features.0.0 + features.0.1 fused)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;
-//                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16);
-//                  fused SE excitation (the block's SE_FC folded in): p5 fc1 w [S][C]; p6 fc1 b; p7 fc2 w^T
-//                  [S][C]; p8 fc2 b; p9 scale [B,C] | 0; p10 tickets int [B] (zero between forwards);
-//                  i11 S; i12 squeezed pixels Ho*Wo
+//                  i0..9 B,H,W,C,Ho,Wo,K,stride,pad,act; i10 SE partial-sum splits (0 = 16)
 //   MBCONV         InvertedResidual without SE in one kernel: p0 x; p1 expand w [Cexp][i12]; p2 b1;
 //                  p3 dw w [K*K][Cexp]; p4 bd; p5 project w [Cout][i13]; p6 b2; p7 y;
 //                  i0..11 B,H,W,Cin,Cexp,Cout,Ho,Wo,K,stride,pad,act; i14 residual
@@ -151,14 +148,6 @@ static DwParams dw_params(const edgedet_op& o) {
     p.pad = (int)I[8];
     p.act = (int)I[9];
     p.parts = I[10] > 0 ? (int)I[10] : SE_PARTS;
-    p.se_w1 = P<const float>(o, 5);  // fused SE excitation (p9 = the scale it writes), or null
-    p.se_b1 = P<const float>(o, 6);
-    p.se_w2t = P<const float>(o, 7);
-    p.se_b2 = P<const float>(o, 8);
-    p.se_scale = P<float>(o, 9);
-    p.se_count = P<int>(o, 10);
-    p.se_S = (int)I[11];
-    p.se_HW = (int)I[12];
     return p;
 }
 

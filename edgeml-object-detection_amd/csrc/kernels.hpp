@@ -54,17 +54,6 @@ struct DwParams {
     float* part;     // optional SE squeeze partial sums [B][parts][C]
     int B, H, W, C, Ho, Wo, K, stride, pad, act;
     int parts;       // pixel splits of the squeeze (1..SE_PARTS)
-    // optional SqueezeExcitation excitation fused into the squeeze (se_scale != null): the last
-    // workgroup of each image to publish its partial sums computes scale[b][C] = hardsigmoid(fc2(
-    // relu(fc1(mean)))) -- the SE_FC launch of the block is gone.  se_count: [B] arrival tickets,
-    // zero between forwards (the last arriver resets its image's).
-    const float* se_w1;   // [S][C]
-    const float* se_b1;   // [S]
-    const float* se_w2t;  // [S][C] (fc2 transposed)
-    const float* se_b2;   // [C]
-    float* se_scale;      // [B][C]
-    int* se_count;        // [B]
-    int se_S, se_HW;
 };
 
 // Up to EDGEDET_MAX_GROUP depthwise problems issued as one launch (dwconv_group_launch).

@@ -87,7 +87,6 @@ int preprocess_launch(const PreParams& p0, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------ depthwise
-constexpr int SE_CMAX_DW = 1024, SE_SMAX_DW = 512;  // fused excitation limits (channels, squeeze)
 
 __global__ void dwconv_kernel(DwParams p) {
     const int C4 = p.C >> 2;
@@ -262,65 +261,6 @@ __global__ void __launch_bounds__(256) dwconv_rb_group_kernel(DwGroup g) {
     dwconv_rb_body<K, S, PW>(g.p[k], g.nq[k], g.nwg[k], (int64_t)(bx - g.start[k]) * blockDim.x + threadIdx.x);
 }
 
-// SqueezeExcitation excitation by the image's last workgroup (DwParams.se_scale).  Every workgroup of
-// image b has stored its squeeze partial sums; it publishes them at agent scope (the last arriver may
-// sit on another XCD: MI355X_MICROARCH.md, inter-workgroup visibility -- every wave drains its stores,
-// the workgroup barrier, one agent release, the ticket) and takes a ticket; the workgroup that draws
-// the last ticket acquires, reduces the partial sums to the channel means, and runs fc1 + ReLU and
-// fc2 + Hardsigmoid in se_fused_kernel's arithmetic order (4-lane C-quarter dot products, sequential
-// over S), writing scale[b][C] for the projection conv; it then resets the ticket for the next forward.
-__device__ void se_excite_last(const DwParams& p, int b) {
-    __shared__ int last;
-    __shared__ float ms[SE_CMAX_DW];
-    __shared__ float hs[SE_SMAX_DW];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int total = (int)(gridDim.x * gridDim.y);
-        last = atomicAdd(p.se_count + b, 1) == total - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (!last) return;
-    const int C = p.C, S = p.se_S;
-    const float inv = 1.f / (float)p.se_HW;
-    const float* pb = p.part + (int64_t)b * p.parts * C;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        float acc = 0.f;
-        for (int k = 0; k < p.parts; ++k) acc += pb[(int64_t)k * C + c];
-        ms[c] = acc * inv;
-    }
-    __syncthreads();
-    const int ch = (C + 3) >> 2;
-    for (int o = threadIdx.x >> 2; o < S; o += blockDim.x >> 2) {
-        const int h = threadIdx.x & 3;
-        const int c0 = h * ch, c1 = min(C, c0 + ch);
-        const float* wr = p.se_w1 + (int64_t)o * C;
-        float acc = 0.f;
-#pragma unroll 8
-        for (int cc = c0; cc < c1; ++cc) acc = fmaf(wr[cc], ms[cc], acc);
-        acc += __shfl_xor(acc, 1);
-        acc += __shfl_xor(acc, 2);
-        if (h == 0) {
-            const float t = acc + p.se_b1[o];
-            hs[o] = t > 0.f ? t : 0.f;
-        }
-    }
-    __syncthreads();
-    for (int cc = threadIdx.x; cc < C; cc += blockDim.x) {
-        float a = 0.f;
-#pragma unroll 8
-        for (int j = 0; j < S; ++j) a = fmaf(p.se_w2t[(int64_t)j * C + cc], hs[j], a);
-        p.se_scale[(int64_t)b * C + cc] = apply_act(a + p.se_b2[cc], ACT_HSIGMOID);
-    }
-    if (threadIdx.x == 0) p.se_count[b] = 0;  // every workgroup of the image has arrived
-}
-
 template <int K, int S, int PW>
 __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, int nwg) {
     __shared__ f32x4 red[16][16];
@@ -361,7 +301,6 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
         for (int k = 1; k < 16; ++k) t += red[k][ql];
         *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * p.parts + sidx) * p.C + c) = t;
     }
-    if (p.se_scale) se_excite_last(p, b);
 }
 
 template <int K, int S>
@@ -888,14 +827,6 @@ int dwconv_launch(const DwParams& p, hipStream_t s) {
     EDGEDET_REQUIRE(p.x && p.w && p.bias && p.y, "dwconv: null x/w/bias/y");
     EDGEDET_REQUIRE(p.C % 4 == 0, "dwconv: C must be a multiple of 4");
     if (p.part) EDGEDET_REQUIRE(p.parts >= 1 && p.parts <= SE_PARTS, "dwconv: 1..16 SE partial sums");
-    if (p.se_scale) {
-        EDGEDET_REQUIRE(p.part && p.se_w1 && p.se_b1 && p.se_w2t && p.se_b2 && p.se_count,
-                        "dwconv: fused SE excitation needs the partial sums, fc weights and tickets");
-        EDGEDET_REQUIRE(p.C <= SE_CMAX_DW && p.se_S >= 1 && p.se_S <= SE_SMAX_DW && p.se_HW >= 1,
-                        "dwconv: fused SE excitation: C <= 1024, 1 <= S <= 512");
-        EDGEDET_REQUIRE((p.K == 3 || p.K == 5) && (p.stride == 1 || p.stride == 2),
-                        "dwconv: fused SE excitation on the register-blocked shapes (K 3 / 5, stride 1 / 2)");
-    }
     if (p.K == 3 && p.stride == 1) return dwconv_rb_launch<3, 1>(p, s);
     if (p.K == 3 && p.stride == 2) return dwconv_rb_launch<3, 2>(p, s);
     if (p.K == 5 && p.stride == 1) return dwconv_rb_launch<5, 1>(p, s);

@@ -680,7 +680,6 @@ class SSDLite {
         struct DwOut {
             Cur y;
             int part = -1, parts = 0;
-            size_t op = 0;  // the DWCONV record (the SE excitation is fused into it)
         };
         auto dw = [&](const Cur& in, const std::string& prefix, int k, int stride, int act, bool se_part) {
             const int64_t C = in.s[3];
@@ -703,7 +702,7 @@ class SSDLite {
             o.p[3] = P.ref(y);
             o.p[4] = part >= 0 ? P.ref(part) : Ref();
             P.add(o);
-            return DwOut{Cur{P.ref(y), ys}, part, parts, P.ops.size() - 1};
+            return DwOut{Cur{P.ref(y), ys}, part, parts};
         };
         auto se = [&](const DwOut& in, const std::string& p) {
             const int64_t C = in.y.s[3];
@@ -711,18 +710,20 @@ class SSDLite {
             WRef w1, b1, w2t, b2;
             se_weights(p, C, sq, w1, b1, w2t, b2);
             const int scale = P.buf({B, C}, 4, p + ".scale" + sfx);
-            // the excitation runs in the depthwise launch (its last workgroup per image, fused into the
-            // squeeze): no SE_FC record; per-image arrival tickets, zero from the workspace's prepare
-            const int tickets = P.buf({B}, I32, p + ".tickets" + sfx);
-            OpRec& o = P.ops[in.op];
-            o.p[5] = Plan::wref(w1);
-            o.p[6] = Plan::wref(b1);
-            o.p[7] = Plan::wref(w2t);
-            o.p[8] = Plan::wref(b2);
-            o.p[9] = P.ref(scale);
-            o.p[10] = P.ref(tickets);
-            o.i[11] = sq;
-            o.i[12] = in.y.s[1] * in.y.s[2];
+            const int hidden = P.buf({B, sq}, 4, p + ".hidden" + sfx);
+            OpRec o;
+            o.kind = EDGEDET_OP_SE_FC;
+            o.name = p;
+            const int64_t iv[5] = {B, C, sq, in.y.s[1] * in.y.s[2], in.parts};
+            for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
+            o.p[0] = P.ref(in.part);
+            o.p[1] = Plan::wref(w1);
+            o.p[2] = Plan::wref(b1);
+            o.p[3] = Plan::wref(w2t);
+            o.p[4] = Plan::wref(b2);
+            o.p[5] = P.ref(scale);
+            o.p[6] = P.ref(hidden);
+            P.add(o);
             return P.ref(scale);
         };
         auto mb_block = [&](const Cur& in, const Block& b, const Prefixes& pf) {

@@ -449,47 +449,3 @@ def test_mbconv_block_matches_torch(B, H, W, Cin, E, Cout, k, s, act):
     got = yd.cpu()
     err = (got - ref).abs().max().item()
     assert torch.isfinite(got).all() and err <= 1e-4 * max(1.0, ref.abs().max().item()), err
-
-
-@pytest.mark.parametrize("B,H,W,C,S,k,s", [(16, 40, 40, 120, 32, 5, 1), (16, 20, 20, 672, 168, 3, 1),
-                                            (3, 20, 20, 672, 168, 5, 2), (2, 10, 10, 480, 120, 5, 1)])
-def test_dwconv_fused_se_excitation(B, H, W, C, S, k, s):
-    """The SqueezeExcitation excitation fused into the depthwise squeeze (DWCONV record with p5..p10:
-    the image's last workgroup computes scale = hardsigmoid(fc2(relu(fc1(mean(y)))))) against torch
-    fp32, replayed three times (the arrival tickets must reset between forwards), on the SSDLite SE
-    shapes."""
-    import ctypes
-    from edgeml_amd import ops
-    from edgeml_amd.plan import pack_dw_weight
-    g = torch.Generator().manual_seed(C + S)
-    x = torch.randn(B, C, H, W, generator=g)
-    w = torch.randn(C, 1, k, k, generator=g) / k
-    b = torch.randn(C, generator=g) * 0.1
-    w1, b1 = torch.randn(S, C, generator=g) / C ** 0.5, torch.randn(S, generator=g) * 0.1
-    w2, b2 = torch.randn(C, S, generator=g) / S ** 0.5, torch.randn(C, generator=g) * 0.1
-    y_ref = F.relu(F.conv2d(x, w, b, s, (k - 1) // 2, 1, C))
-    m = y_ref.mean((2, 3))
-    scale_ref = F.hardsigmoid(F.linear(F.relu(F.linear(m, w1, b1)), w2, b2))
-    Ho, Wo = y_ref.shape[-2:]
-    parts = ops.se_parts(Ho, Wo)
-    d = lambda t: t.contiguous().to(DEV)  # noqa: E731
-    xd, wd, bd = d(x.permute(0, 2, 3, 1)), d(torch.from_numpy(pack_dw_weight(w.numpy()))), d(b)
-    y = torch.zeros(B, Ho, Wo, C, device=DEV)
-    part = torch.zeros(B, parts, C, device=DEV)
-    w1d, b1d, w2td, b2d = d(w1), d(b1), d(w2.t()), d(b2)
-    scale = torch.zeros(B, C, device=DEV)
-    tickets = torch.zeros(B, dtype=torch.int32, device=DEV)
-    r = np.zeros(1, dtype=ops.OP_DTYPE)
-    r[0]["kind"] = ops.DWCONV
-    for j, v in enumerate((B, H, W, C, Ho, Wo, k, s, (k - 1) // 2, ops.ACT["RE"], parts, S, Ho * Wo)):
-        r[0]["i"][j] = v
-    for j, t in enumerate((xd, wd, bd, y, part, w1d, b1d, w2td, b2d, scale, tickets)):
-        r[0]["p"][j] = t.data_ptr()
-    for _ in range(3):
-        scale.zero_()
-        ops.check(ops.lib().edgedet_plan_run(r.ctypes.data_as(ctypes.c_void_p), 1, ops.stream_handle()))
-        torch.cuda.synchronize()
-        assert (y.permute(0, 3, 1, 2).cpu() - y_ref).abs().max().item() < 1e-5
-        err = (scale.cpu() - scale_ref).abs().max().item()
-        assert err < 1e-5, err
-        assert int(tickets.abs().sum().item()) == 0  # reset by every image's last workgroup

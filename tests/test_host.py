@@ -172,10 +172,7 @@ def test_ssd_plan_lowering():
     heads = 12
     assert n_dw == 15 + 4 + heads - stem - mb
     assert n_conv == 1 + 23 + 2 + 4 + 1 + 8 + heads - 2 * stem - 2 * mb
-    # the SE excitations run inside their depthwise launches (fused squeeze + excitation): no SE_FC
-    assert kinds.count(ops.SE_FC) == 0
-    se = [op for op in P.ops if op.kind == ops.DWCONV and op.p.get(9) is not None]
-    assert len(se) == 8 and all(op.i[11] > 0 and op.p.get(10) is not None for op in se)
+    assert kinds.count(ops.SE_FC) == 8
     assert m.grids == [(20, 20), (10, 10), (5, 5), (3, 3), (2, 2), (1, 1)]
     for op in P.ops:
         if op.kind == ops.CONV:
@@ -332,11 +329,10 @@ def test_bench_attaches_committed_pmc_traffic():
         pmc = json.load(f)
     base = pmc["launch"].split("#")[0]
     for k in (0, 1):
-        roof = {"launch": f"{base}#{k}", "grid_wg": pmc["grid_wg"], "traffic": None, "kernel": pmc["kernel"]}
+        roof = {"launch": f"{base}#{k}", "grid_wg": pmc["grid_wg"], "traffic": None, "_op_index": 3}
         bench.attach_traffic(roof, "ssd")
-        assert roof["traffic"] == pmc["hbm_bytes_per_launch"]
+        assert roof["traffic"] == pmc["hbm_bytes_per_launch"] and "_op_index" not in roof
     for roof in ({"launch": base + "#0", "grid_wg": pmc["grid_wg"] + 1, "traffic": None},
-                 {"launch": "backbone.features.0.0#0", "grid_wg": pmc["grid_wg"], "traffic": None},
-                 {"launch": base + "#0", "grid_wg": pmc["grid_wg"], "traffic": None, "kernel": "other_kernel"}):
+                 {"launch": "backbone.features.0.0#0", "grid_wg": pmc["grid_wg"], "traffic": None}):
         bench.attach_traffic(roof, "ssd")
         assert roof["traffic"] is None

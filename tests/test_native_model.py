@@ -87,17 +87,12 @@ def test_ssd_packing_matches_restatement(built, rt):
     np.testing.assert_array_equal(_blob_f32(m, op.p[4], bd.size), bd)
     p = "head.classification_head.module_list.0.1"  # 1x1 with bias, no BN
     _check_conv(m, _op(P, p), s(p + ".weight").astype(np.float32), s(p + ".bias"))
-    # SqueezeExcitation block.2, fused into the depthwise record of block.1: fc1 [S][C] (p5), fc1 bias
-    # (p6), fc2 transposed [S][C] (p7), fc2 bias (p8); i3 = C, i11 = S
-    p = "backbone.features.0.4.block.2"
-    op = _op(P, "backbone.features.0.4.block.1")
-    C, S = op.i[3], op.i[11]
-    assert S == s(p + ".fc1.weight").shape[0] and op.i[12] == op.i[4] * op.i[5]
-    np.testing.assert_array_equal(_blob_f32(m, op.p[5], S * C), s(p + ".fc1.weight").astype(np.float32).reshape(-1))
-    np.testing.assert_array_equal(_blob_f32(m, op.p[6], S), s(p + ".fc1.bias").astype(np.float32))
-    np.testing.assert_array_equal(_blob_f32(m, op.p[7], S * C),
+    p = "backbone.features.0.4.block.2"  # SqueezeExcitation: fc1 [S][C], fc2 transposed [S][C]
+    op = _op(P, p)
+    C, S = op.i[1], op.i[2]
+    np.testing.assert_array_equal(_blob_f32(m, op.p[1], S * C), s(p + ".fc1.weight").astype(np.float32).reshape(-1))
+    np.testing.assert_array_equal(_blob_f32(m, op.p[3], S * C),
                                   s(p + ".fc2.weight")[:, :, 0, 0].T.astype(np.float32).reshape(-1))
-    np.testing.assert_array_equal(_blob_f32(m, op.p[8], C), s(p + ".fc2.bias").astype(np.float32))
 
 
 def test_frcnn_packing_matches_restatement(built):
