@@ -73,6 +73,7 @@ def step(plan, stream, d2h):
 
 
 TIMING = {}  # how the last timed_steps call measured (reported on the JSON line)
+SETTLE_S = 0.5  # untimed device warm-up before the warmup passes (seconds of wall time)
 
 
 def timed_steps(plan, stream, steps, warmup, dist, extra=()):
@@ -98,6 +99,16 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    # settle: untimed passes for SETTLE_S of wall time before the warmup, so the timed passes run at the
+    # clocks a long run holds (the first ~30 ms after an idle host phase ran 15-20 % slower on the box:
+    # profiles/r4a_bench_driver.json 1.67 ms/step at 20 steps against 1.38 in a 750-step run)
+    t_settle, settled = time.perf_counter(), 0
+    while time.perf_counter() - t_settle < SETTLE_S:
+        for i in range(2 * n):
+            step(*lanes[i % n])
+        settled += 2 * n
+        for _, s_, _ in lanes:
+            s_.synchronize()
     for i in range(warm):
         step(*lanes[i % n])
     mark = torch.cuda.Event(enable_timing=True)
@@ -124,7 +135,7 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     TIMING.update({"method": "steady state: K pass completions (HIP events after each pass's D2H) from the "
                              "last warmup completion; pipeline kept full across the start",
                    "device_s": round(el, 6), "wall_s_incl_drain": round(wall, 6), "warmup_passes": warm,
-                   "instances": n})
+                   "settle_passes": settled, "instances": n})
     return el
 
 
@@ -440,7 +451,8 @@ def attach_traffic(roof, model):
     # "#k" names the k-th batch chain's copy of a layer: the chains split the batch evenly, so
     # every copy has the same shape and grid and one PMC summary covers them all
     same = lambda a: (a or "").split("#")[0]
-    if same(pmc.get("launch")) == same(roof.get("launch")) and pmc.get("grid_wg") == roof.get("grid_wg"):
+    kernel_ok = not (pmc.get("kernel") and roof.get("kernel")) or pmc["kernel"] == roof["kernel"]
+    if same(pmc.get("launch")) == same(roof.get("launch")) and pmc.get("grid_wg") == roof.get("grid_wg") and kernel_ok:
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["traffic_source"] = os.path.relpath(path, ROOT)
 

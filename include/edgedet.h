@@ -39,8 +39,7 @@ extern "C" {
 #define EDGEDET_OP_FLTS 16
 
 /* One op record.  Field layouts per kind: csrc/exec.hip (header comment), e.g. DWCONV p0 x, p1 w,
- * p2 bias, p3 y, p4 SE partial sums, p5..p10 fused SE excitation (fc1 w, fc1 b, fc2 w^T, fc2 b,
- * scale out, per-image tickets); GROUP i0 = members. */
+ * p2 bias, p3 y, p4 SE partial sums; GROUP i0 = members. */
 typedef struct edgedet_op {
     int64_t kind;
     int64_t i[EDGEDET_OP_INTS];
@@ -53,8 +52,7 @@ enum {
     EDGEDET_OP_MEMSET = 1,        /* zero p[0] for i[0] bytes                                         */
     EDGEDET_OP_PREPROCESS = 2,    /* GeneralizedRCNNTransform: normalize, bilinear resize, zero pad   */
     EDGEDET_OP_CONV = 3,          /* conv2d + folded BN + bias + residual/upsample-add + activation   */
-    EDGEDET_OP_DWCONV = 4,        /* depthwise conv2d + folded BN + activation (+ the SE squeeze; with
-                                   * p5..p10 also the SE excitation, by each image's last workgroup)   */
+    EDGEDET_OP_DWCONV = 4,        /* depthwise conv2d + folded BN + activation (+ the SE squeeze)      */
     EDGEDET_OP_CHANNEL_MEAN = 5,  /* adaptive_avg_pool2d(1) (SqueezeExcitation squeeze)               */
     EDGEDET_OP_SE_FC = 6,         /* SqueezeExcitation fc1-ReLU-fc2-Hardsigmoid (standalone form)      */
     EDGEDET_OP_MAXPOOL = 7,       /* max_pool2d (ResNet stem 3x3 s2 p1, FPN LastLevelMaxPool 1x1 s2)  */

@@ -43,6 +43,8 @@ def test_engine_orie_no_further_from_f64_than_the_f32_oracle():
     fx = {k: _sets(z, k, N) for k in ("weak_f64", "strong_f64", "weak_f32", "strong_f32")}
     with tempfile.TemporaryDirectory() as td:
         d = lambda *p: os.path.join(td, *p)  # noqa: E731
+        for sub in ("eng_weak", "eng_strong", "f64_weak", "f64_strong", "f32_weak", "f32_strong", "labels"):
+            os.makedirs(d(sub))
         for i in range(N):
             img = synthetic.make_batch(1, 640, 640, seed=int(z["seeds"][i]))
             assert float(img.double().sum()) == float(z["image_sums"][i]), "regenerated input differs from G5's"
@@ -54,7 +56,6 @@ def test_engine_orie_no_further_from_f64_than_the_f32_oracle():
                 fmt.save_npy(d("f64_" + tag), name, fx[tag + "_f64"][i])
                 fmt.save_npy(d("f32_" + tag), name, fx[tag + "_f32"][i])
             rows = fx["strong_f64"][i]
-            os.makedirs(d("labels"), exist_ok=True)
             with open(d("labels", name[:-4] + ".txt"), "w") as f:
                 for r in rows[rows[:, 5] >= 0.3]:
                     f.write(" ".join([str(int(r[0]))] + [repr(float(v)) for v in r[1:5]]) + "\n")

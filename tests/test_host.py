@@ -329,10 +329,11 @@ def test_bench_attaches_committed_pmc_traffic():
         pmc = json.load(f)
     base = pmc["launch"].split("#")[0]
     for k in (0, 1):
-        roof = {"launch": f"{base}#{k}", "grid_wg": pmc["grid_wg"], "traffic": None, "_op_index": 3}
+        roof = {"launch": f"{base}#{k}", "grid_wg": pmc["grid_wg"], "traffic": None, "kernel": pmc["kernel"]}
         bench.attach_traffic(roof, "ssd")
-        assert roof["traffic"] == pmc["hbm_bytes_per_launch"] and "_op_index" not in roof
+        assert roof["traffic"] == pmc["hbm_bytes_per_launch"]
     for roof in ({"launch": base + "#0", "grid_wg": pmc["grid_wg"] + 1, "traffic": None},
-                 {"launch": "backbone.features.0.0#0", "grid_wg": pmc["grid_wg"], "traffic": None}):
+                 {"launch": "backbone.features.0.0#0", "grid_wg": pmc["grid_wg"], "traffic": None},
+                 {"launch": base + "#0", "grid_wg": pmc["grid_wg"], "traffic": None, "kernel": "other_kernel"}):
         bench.attach_traffic(roof, "ssd")
         assert roof["traffic"] is None
