@@ -852,7 +852,9 @@ class SSDLite {
             off += f.s[1] * f.s[2] * 6;
         }
         const int ng = (int)hops.size();
+        const bool hgroup = env_int("EDGEDET_HEAD_GROUP", 1) == 1;  // A/B switch (temporary, round 4)
         auto group = [&](const std::string& name) {
+            if (!hgroup) return;
             OpRec g;
             g.kind = EDGEDET_OP_GROUP;
             g.name = name + sfx;
@@ -878,7 +880,7 @@ class SSDLite {
             a.y_pstride = 6 * h.cols;
             a.y_bstride = A * h.cols;
             a.y_off = (int64_t)img0 * A * h.cols + h.off * h.cols;
-            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") ? 0 : HEAD_TILE;  // f32: the members run alone
+            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") || !hgroup ? 0 : HEAD_TILE;  // f32: the members run alone
             a.name = h.p + ".1" + sfx;
             conv_op(P, a);
         }

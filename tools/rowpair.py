@@ -47,7 +47,7 @@ def compare_dirs(names, load_a, load_b):
     """Aggregate identity-paired differences over images.  load_a / load_b: name -> rows."""
     out = {"images": len(names), "files_identical": 0, "paired": 0, "unpaired_a": 0, "unpaired_b": 0,
            "images_with_unpaired": 0, "max_paired_dconf": 0.0, "max_paired_dbox": 0.0,
-           "max_unpaired_conf": 0.0, "order_differs": 0}
+           "max_unpaired_conf": 0.0, "order_differs": 0, "paired_dconf_gt_1e-4": 0, "paired_dconf_gt_1e-3": 0}
     for n in names:
         a, b = load_a(n), load_b(n)
         if a.shape == b.shape and np.array_equal(a, b):
@@ -59,7 +59,10 @@ def compare_dirs(names, load_a, load_b):
         out["images_with_unpaired"] += bool(len(ua) or len(ub))
         if pairs:
             i, j = np.array(pairs).T
-            out["max_paired_dconf"] = max(out["max_paired_dconf"], float(np.abs(a[i, 5] - b[j, 5]).max()))
+            dc = np.abs(a[i, 5] - b[j, 5])
+            out["max_paired_dconf"] = max(out["max_paired_dconf"], float(dc.max()))
+            out["paired_dconf_gt_1e-4"] += int(np.count_nonzero(dc > 1e-4))
+            out["paired_dconf_gt_1e-3"] += int(np.count_nonzero(dc > 1e-3))
             out["max_paired_dbox"] = max(out["max_paired_dbox"], float(np.abs(a[i, 1:5] - b[j, 1:5]).max()))
             # the same detections in a different row order (two near-equal scores traded places)
             out["order_differs"] += bool(not np.array_equal(np.argsort(i, kind="stable"), np.argsort(j, kind="stable")))
