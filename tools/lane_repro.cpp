@@ -6,7 +6,11 @@
 // EVENTS, or both, or nothing; then launches the graph three times and checks the kernels' output.
 // Plain HIP runtime, no library, one variant per process:
 //
-//   lane_repro none|events|streams|both
+//   lane_repro none|events|streams|both                 (destroyed after instantiate + upload)
+//   lane_repro streams_during|events_during             (destroyed after the JOIN, BEFORE
+//                                                         hipStreamEndCapture: the round-3 library
+//                                                         released a run's lane set when run_ops
+//                                                         returned, inside the capture)
 //
 // Exit 0 = the graph ran and the results are right after the destruction; 2 = wrong results; 3 = a
 // HIP error.  A segfault shows as the process dying (status 139 from the shell).
@@ -36,6 +40,7 @@ int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "none";
     const bool kill_streams = !strcmp(mode, "streams") || !strcmp(mode, "both");
     const bool kill_events = !strcmp(mode, "events") || !strcmp(mode, "both");
+    const bool during_streams = !strcmp(mode, "streams_during"), during_events = !strcmp(mode, "events_during");
     constexpr int N = 1 << 16, SIDE = 2;
     float* buf = nullptr;
     CK(hipMalloc(&buf, sizeof(float) * N * (SIDE + 1)));
@@ -60,6 +65,12 @@ int main(int argc, char** argv) {
     for (int l = 0; l < SIDE; ++l) {  // JOIN
         CK(hipEventRecord(join_ev[l], side[l]));
         CK(hipStreamWaitEvent(s, join_ev[l], 0));
+    }
+    if (during_streams)
+        for (int l = 0; l < SIDE; ++l) CK(hipStreamDestroy(side[l]));
+    if (during_events) {
+        CK(hipEventDestroy(fork_ev));
+        for (int l = 0; l < SIDE; ++l) CK(hipEventDestroy(join_ev[l]));
     }
     CK(hipStreamEndCapture(s, &graph));
     CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
