@@ -99,24 +99,29 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    # settle: untimed passes for SETTLE_S of wall time before the warmup, so the timed passes run at the
-    # clocks a long run holds (the first ~30 ms after an idle host phase ran 15-20 % slower on the box:
-    # profiles/r4a_bench_driver.json 1.67 ms/step at 20 steps against 1.38 in a 750-step run)
-    t_settle, settled = time.perf_counter(), 0
-    while time.perf_counter() - t_settle < SETTLE_S:
-        for i in range(2 * n):
-            step(*lanes[i % n])
-        settled += 2 * n
-        for _, s_, _ in lanes:
-            s_.synchronize()
+    # settle: untimed passes for SETTLE_S of wall time before the warmup, issued like the timed ones
+    # (round robin, never drained: the host waits only for the pass 2n back, so the instances keep the
+    # staggered phases of a long run instead of starting in lockstep) -- the clocks and the overlap the
+    # timed passes see are a long run's (profiles/r4a_bench_driver.json: 1.67 ms/step over 20 steps
+    # right after an idle host phase, against 1.38 in a 750-step run)
+    t_settle, settled, ring = time.perf_counter(), 0, []
+    while time.perf_counter() - t_settle < SETTLE_S or settled < 2 * n:
+        p_, s_, d_ = lanes[settled % n]
+        step(p_, s_, d_)
+        e = torch.cuda.Event()
+        e.record(s_)
+        ring.append(e)
+        if len(ring) > 2 * n:
+            ring.pop(0).synchronize()
+        settled += 1
     for i in range(warm):
-        step(*lanes[i % n])
+        step(*lanes[(settled + i) % n])
     mark = torch.cuda.Event(enable_timing=True)
-    mark.record(lanes[(warm - 1) % n][1])
+    mark.record(lanes[(settled + warm - 1) % n][1])
     done = []
     t0 = time.perf_counter()
     for i in range(steps):
-        p, s, d2h = lanes[(warm + i) % n]
+        p, s, d2h = lanes[(settled + warm + i) % n]
         step(p, s, d2h)
         e = torch.cuda.Event(enable_timing=True)
         e.record(s)

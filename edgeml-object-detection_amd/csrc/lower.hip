@@ -830,7 +830,8 @@ class SSDLite {
         // the reg branch.  The weights are packed in the module order (map, branch); the records run as
         // two grouped launches (EDGEDET_OP_GROUP): the twelve depthwise convs, then the twelve 1x1
         // convs, which store straight into the concatenated head tensors (pixel stride 6 * cols, map
-        // anchor offset) -- 24 sequential launches per chain become 2.
+        // anchor offset) -- 24 sequential launches per chain become 2: SSD 28.97k / 28.71k -> 30.75k / 30.84k
+        // img/s (alternated 750-step runs, profiles/r4b_ab_heads.txt).
         struct HeadOp {
             std::string p;
             int64_t cols, off;
@@ -852,9 +853,7 @@ class SSDLite {
             off += f.s[1] * f.s[2] * 6;
         }
         const int ng = (int)hops.size();
-        const bool hgroup = env_int("EDGEDET_HEAD_GROUP", 1) == 1;  // A/B switch (temporary, round 4)
         auto group = [&](const std::string& name) {
-            if (!hgroup) return;
             OpRec g;
             g.kind = EDGEDET_OP_GROUP;
             g.name = name + sfx;
@@ -880,7 +879,7 @@ class SSDLite {
             a.y_pstride = 6 * h.cols;
             a.y_bstride = A * h.cols;
             a.y_off = (int64_t)img0 * A * h.cols + h.off * h.cols;
-            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") || !hgroup ? 0 : HEAD_TILE;  // f32: the members run alone
+            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") ? 0 : env_int("EDGEDET_HEAD_TILE", HEAD_TILE);  // f32: alone
             a.name = h.p + ".1" + sfx;
             conv_op(P, a);
         }
