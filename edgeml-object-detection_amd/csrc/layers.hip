@@ -337,7 +337,7 @@ constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 
 // T = float: the transform's NHWC4 output (p.x); T = float / uint8_t with FUSED: the source image
 // (p.src / p.src8, [B][3][H0][W0]) and the transform computed per input pixel of the tile (pre_pixel,
 // the same bits as the transform kernel): no transform launch and no NHWC4 round trip through HBM.
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, bool MF>
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
@@ -384,6 +384,36 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
         for (int r = 0; r < STEM_NW / 256; ++r) ws[tid + 256 * r] = wv[r];
     }
     __syncthreads();
+    const int lane = tid & 63, wid = tid >> 6, l16 = lane & 15, q4 = lane >> 4;
+    if constexpr (MF) {
+        // stem conv as a GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32 products): rows =
+        // the 324 halo pixels in 21 tiles of 16 (wave w takes tiles w, w + 4, ...), columns = the 16
+        // output channels, K = 9 taps x 4 channels in the packed (kh, kw, ci) order (one MFMA per tap)
+        float wb[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wb[t] = ws[STEM_W0 + l16 * 36 + 4 * t + q4];
+        const float b0v = ws[STEM_B0 + l16];
+        constexpr int NV = STEM_SH * STEM_SH, NTL = (NV + 15) / 16;
+        for (int tl = wid; tl < NTL; tl += 4) {
+            const int va = min(16 * tl + l16, NV - 1);  // this lane's A row (pad rows repeat the last pixel)
+            const int lh = va / STEM_SH, lw = va - lh * STEM_SH;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float av = xs[4 * ((2 * lh + t / 3) * STEM_XH + 2 * lw + t % 3) + q4];
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[t], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int v = 16 * tl + 4 * q4 + i;
+                if (v < NV) {
+                    const int vh = v / STEM_SH, vw = v - vh * STEM_SH;
+                    const bool in = (unsigned)(sh0 + vh) < (unsigned)p.Ho && (unsigned)(sw0 + vw) < (unsigned)p.Wo;
+                    ss[v * STEM_SS + l16] = in ? apply_act(acc[i] + b0v, ACT_HSWISH) : 0.f;
+                }
+            }
+        }
+    } else
     for (int v = tid; v < STEM_SH * STEM_SH; v += 256) {
         asm volatile("" ::: "memory");  // keep the weight reads in the loop (hoisted, they took 256 VGPRs)
         const int lh = v / STEM_SH, lw = v % STEM_SH;
@@ -410,6 +440,52 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
     __syncthreads();
     const int lh = tid / STEM_T, lw = tid % STEM_T;
     const int oh = oh0 + lh, ow = ow0 + lw;
+    if constexpr (MF) {
+        // depthwise on the vector ALUs (one output pixel x 16 channels per thread, taps (kh, kw)), its
+        // outputs through LDS (the input tile's space, free now) into the projection GEMM on the matrix
+        // cores: rows = the wave's 64 pixels in 4 tiles, columns = 16 channels, K = 16 in 4 steps
+        float dv[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dv[c] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            if ((unsigned)(oh - 1 + kh) >= (unsigned)p.Ho) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const float* sv = ss + ((lh + kh) * STEM_SH + lw + kw) * STEM_SS;
+                const float* wv = ws + STEM_WD + (kh * 3 + kw) * 16;
+#pragma unroll
+                for (int c = 0; c < 16; ++c) dv[c] = fmaf(sv[c], wv[c], dv[c]);
+            }
+        }
+        constexpr int DS = 17;  // odd pitch
+        float* dsm = xs;        // [256][DS]
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dsm[tid * DS + c] = apply_act(dv[c] + ws[STEM_BD + c], ACT_RELU);
+        float w1v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w1v[k] = ws[STEM_W1 + l16 * 16 + 4 * k + q4];
+        const float b1v = ws[STEM_B1 + l16];
+        __syncthreads();
+#pragma unroll
+        for (int tl = 0; tl < 4; ++tl) {
+            const int row0 = 64 * wid + 16 * tl;  // the tile's first output pixel (= thread index)
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dsm[(row0 + l16) * DS + 4 * k + q4], w1v[k], acc, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int px = row0 + 4 * q4 + i, ph = px / STEM_T, pw = px % STEM_T;
+                const int yh = oh0 + ph, yw = ow0 + pw;
+                if (yh < p.Ho && yw < p.Wo) {
+                    const float r = ss[((ph + 1) * STEM_SH + pw + 1) * STEM_SS + l16];
+                    p.y[(((int64_t)b * p.Ho + yh) * p.Wo + yw) * 16 + l16] = (acc[i] + b1v) + r;
+                }
+            }
+        }
+        return;
+    }
     if (oh >= p.Ho || ow >= p.Wo) return;
     float dv[16];
 #pragma unroll
@@ -457,12 +533,16 @@ int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
     EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
     const int tiles_w = cdiv(p.Wo, STEM_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B);
-    if (p.src8)
-        hipLaunchKernelGGL((ssd_stem_kernel<uint8_t, true>), grid, dim3(256), 0, s, p, tiles_w);
-    else if (p.src)
-        hipLaunchKernelGGL((ssd_stem_kernel<float, true>), grid, dim3(256), 0, s, p, tiles_w);
-    else
-        hipLaunchKernelGGL((ssd_stem_kernel<float, false>), grid, dim3(256), 0, s, p, tiles_w);
+    // the matrix-core form (stem conv and projection on v_mfma_f32_16x16x4_f32); EDGEDET_STEM_MFMA=0
+    // keeps the vector-ALU form (temporary A/B switch, round 4)
+    static const bool mf = [] {
+        const char* e = std::getenv("EDGEDET_STEM_MFMA");
+        return !(e && e[0] == '0');
+    }();
+    void (*k)(StemParams, int) = p.src8 ? (mf ? ssd_stem_kernel<uint8_t, true, true> : ssd_stem_kernel<uint8_t, true, false>)
+                                 : p.src ? (mf ? ssd_stem_kernel<float, true, true> : ssd_stem_kernel<float, true, false>)
+                                         : (mf ? ssd_stem_kernel<float, false, true> : ssd_stem_kernel<float, false, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, p, tiles_w);
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
