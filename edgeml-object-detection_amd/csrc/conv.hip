@@ -858,18 +858,22 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 *
 // (!UT) the chunks past Cin are zeroed (they meet the zero weight padding).
 // BN = 64 (with BM = 128, the skewed 16x16x32 pipeline and LDS-DMA B only): 4 x 2 waves of 32 x 32
 // for the Cout = 64 layers, which a 128-wide N tile computes half empty; waves 0..3 copy the B rows.
+// BN = 256 (BM = 128, same conditions): 2 x 4 waves of 64 x 64 in the same 144 KiB, so a Cout = 256
+// layer reads each A panel once (the 256 x 128 tile's two N tiles read it twice) and splits half the
+// A elements per MFMA; each wave copies 32 B rows by LDS-DMA.
 template <bool XF, bool UT, bool PS, int BM = 256, int PF = 1, bool P1 = false, int BN = 128>
 __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk) {
     static_assert(!PS || (UT && !XF), "pre-split input: uniform taps, transform applied by the split");
     static_assert(BM == 256 || ((BM == 128 || BM == 64) && !PS), "x6b tiles: 256 x 128, or 128 | 64 x 128 without pre-split input");
     static_assert(!P1 || !PS, "pointwise stages: fp32 input");
     constexpr bool GL = PF != 2;  // B planes by LDS-DMA (needs the one-register-stage loops)
-    static_assert(BN == 128 || (BN == 64 && BM == 128 && GL && !PS), "x6b BN = 64: 128 x 64, LDS-DMA B");
-    constexpr int WM = BN == 64 ? 4 : (BM == 256 ? 4 : 2), WN = 8 / WM, TM = BM / (WM * 32), TN = BN / (WN * 32), NT = 512;
+    static_assert(BN == 128 || ((BN == 64 || BN == 256) && BM == 128 && GL && !PS), "x6b BN = 64 | 256: 128 x BN, LDS-DMA B");
+    constexpr int WM = BN == 64 ? 4 : BN == 256 ? 2 : (BM == 256 ? 4 : 2), WN = 8 / WM;
+    constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32), NT = 512;
     constexpr int AJ = PS ? BM * 4 / NT : BM * BK6B / 4 / NT;  // A rows per thread (2 | 4 f32x4 loads)
     constexpr int AROWS = NT / (PS ? 4 : 8);                   // row step between a thread's A rows
     constexpr int PA = BM * BK6B, PB = BN * BK6B;  // bf16 elements per plane
-    static_assert(3 * BN * BK6B / 8 == 3 * NT || BN == 64, "one B-plane chunk per thread per plane");
+    static_assert(3 * BN * BK6B / 8 == 3 * NT || GL, "register-staged B: one B-plane chunk per thread per plane");
 
     __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * (PA + PB)];
     unsigned short* As = lds;
@@ -956,17 +960,23 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
     };
     auto load_stage = [&](Regs& R, const StageK& sk, int bbuf) {
         const int k0 = sk.k0;
-        if (GL && 16 * wid < BN) {
-            // B by LDS-DMA: wave w copies rows 16w .. 16w+15 of each plane (1 KiB per instruction, lane l
-            // -> the 16-B slot l of the block); the swizzle is applied on the source address
-            const int row = 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ swz_key(row);
-            const int n = n0 + row < p.Cout ? n0 + row : p.Cout - 1;
-            const unsigned short* src = reinterpret_cast<const unsigned short*>(p.w3) + (int64_t)n * p.Kpad + k0 + 8 * lc;
+        if constexpr (GL) {
+            // B by LDS-DMA: wave w copies rows rb + 16w .. rb + 16w + 15 of each plane for every 128-row
+            // block rb (1 KiB per instruction, lane l -> the 16-B slot l of the block); the swizzle is
+            // applied on the source address
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(src + pl * wplane),
-                    (__attribute__((address_space(3))) void*)(Bs + bbuf * 3 * PB + pl * PB + 16 * wid * BK6B), 16, 0, 0);
+            for (int rb = 0; rb < BN; rb += 128) {
+                if (rb + 16 * wid >= BN) break;
+                const int row = rb + 16 * wid + (lane >> 2), pc = lane & 3, lc = pc ^ swz_key(row);
+                const int n = n0 + row < p.Cout ? n0 + row : p.Cout - 1;
+                const unsigned short* src = reinterpret_cast<const unsigned short*>(p.w3) + (int64_t)n * p.Kpad + k0 + 8 * lc;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(src + pl * wplane),
+                        (__attribute__((address_space(3))) void*)(Bs + bbuf * 3 * PB + pl * PB + (rb + 16 * wid) * BK6B), 16,
+                        0, 0);
+            }
         }
         if constexpr (PS) {
             int kh, kw, ci0;
@@ -1547,6 +1557,7 @@ int conv_launch(ConvParams p, int tile, hipStream_t s) {
         case 31: return launch_x6b<64, 1>(p, s);      // 64 x 128, bf16x6, two workgroups per CU
         case 32: return launch_x6b<64, 2>(p, s);      // the same, two register stages
         case 38: return launch_x6b<128, 1, 64>(p, s); // 128 x 64, bf16x6, 32-deep swizzled stages (Cout <= 64 layers)
+        case 39: return launch_x6b<128, 1, 256>(p, s); // 128 x 256: the A panel read once per Cout = 256 layer
         case 26: {                                    // the same, K split in two halves (atomics into zeroed y)
             ConvParams q = p;
             q.ksplit = 2;
@@ -1610,6 +1621,7 @@ int conv_group_launch(const ConvParams* ps, int n, int tile, hipStream_t s) {
         case 29: return launch_x6b_group<128, 128>(gl, s);
         case 31: return launch_x6b_group<64, 128>(gl, s);
         case 38: return launch_x6b_group<128, 64>(gl, s);
+        case 39: return launch_x6b_group<128, 256>(gl, s);
         default: return 1;
     }
 }

@@ -469,6 +469,8 @@ static void conv_op(Plan& P, const ConvArgs& a) {
         auto it = tile_table().find(conv_key(o));
         if (it != tile_table().end() && it->second && (w3 || it->second < 20)) o.i[23] = it->second;
     }
+    // temporary A/B switch (round 4): the Cout = 256 layers of tile 25 on the 128 x 256 tile
+    if (o.i[23] == 25 && a.cout == 256 && env_int("EDGEDET_TILE39", 0) == 1) o.i[23] = 39;
     if (o.i[23] == 26) {
         const bool dense = yp == a.cout && a.y_off == 0 && (a.y_bstride < 0 || a.y_bstride == Ho * Wo * a.cout);
         if (a.act == 0 && a.res.kind == Ref::NONE && dense && w3) {
@@ -1282,7 +1284,7 @@ class FasterRCNN : public ResNetFPN {
             COpt o;
             o.bias_key = "rpn.head.conv.0.0.bias";
             o.name = "rpn.head.conv.0@" + std::to_string(lvl);
-            o.tile = grouped ? RPN_TILE : 0;
+            o.tile = grouped ? env_int("EDGEDET_RPN_TILE", RPN_TILE) : 0;
             t0s.push_back(conv(P, outs[(size_t)lvl], "rpn.head.conv.0.0.weight", 256, 3, 1, A_RE, o));
         }
         if (grouped) rpn_group("rpn.head.conv.1");
@@ -1290,7 +1292,7 @@ class FasterRCNN : public ResNetFPN {
             COpt o;
             o.bias_key = "rpn.head.conv.1.0.bias";
             o.name = "rpn.head.conv.1@" + std::to_string(lvl);
-            o.tile = grouped ? RPN_TILE : 0;
+            o.tile = grouped ? env_int("EDGEDET_RPN_TILE", RPN_TILE) : 0;
             t1s.push_back(conv(P, t0s[(size_t)lvl], "rpn.head.conv.1.0.weight", 256, 3, 1, A_RE, o));
         }
         for (int lvl = 0; lvl < L5; ++lvl) {

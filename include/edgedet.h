@@ -312,8 +312,8 @@ int edgedet_dwconv2d(const float* x, int64_t B, int64_t H, int64_t W, int64_t C,
 
 /* The conv kernel variant (tile id of csrc/conv.hip conv_launch: 1-6 fp32-MFMA LDS tiles, 10-12 and
  * 15 direct pointwise tiles, 13/14/16/17 split-K pointwise tiles, 21-24/27/28 bf16x6 16-deep LDS tiles,
- * 25/26, 29-32 and 38 bf16x6 32-deep swizzled tiles: 256x128 (26 with split K), 128x128, 64x128,
- * 128x64, 33-35 streaming 1x1 tiles for Cin <= 72, Cout <= 96 with dense output rows) that a CONV
+ * 25/26, 29-32, 38 and 39 bf16x6 32-deep swizzled tiles: 256x128 (26 with split K), 128x128, 64x128,
+ * 128x64, 128x256, 33-35 streaming 1x1 tiles for Cin <= 72, Cout <= 96 with dense output rows) that a CONV
  * record would run; negative on error. */
 int edgedet_conv_tile(const edgedet_op* op);
 

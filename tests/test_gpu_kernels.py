@@ -308,7 +308,7 @@ def test_split_bf16x3_device_matches_host():
     assert np.array_equal(got, split_bf16x3(w.numpy()))
 
 
-@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25, 27, 28, 29, 30, 31, 32, 38])
+@pytest.mark.parametrize("tile", [0, 22, 23, 24, 25, 27, 28, 29, 30, 31, 32, 38, 39])
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 7, 8)])
 def test_conv_bf16x6_matches_torch(case, tile):
     _conv_case(*case, tile=tile, x6=True)
@@ -361,7 +361,7 @@ def test_conv_bf16x6_split_k(case):
     assert torch.equal(y1, y2)
 
 
-@pytest.mark.parametrize("tile", [25, 29, 30, 31, 32, 38])
+@pytest.mark.parametrize("tile", [25, 29, 30, 31, 32, 38, 39])
 @pytest.mark.parametrize("se", [False, True])
 @pytest.mark.parametrize("case", [(2, 9, 9, 16, 16, 1, 1, None, True), (3, 11, 7, 24, 72, 1, 1, "HS", False),
                                   (2, 13, 10, 40, 120, 1, 1, "RE", False), (1, 20, 20, 72, 24, 1, 1, None, True)])
@@ -372,7 +372,7 @@ def test_conv_bf16x6_pointwise_ragged_cin(case, se, tile):
     _conv_case(*case, tile=tile, se=se, x6=True)
 
 
-@pytest.mark.parametrize("tile", [22, 23, 24, 25, 29, 30, 31, 32, 38])
+@pytest.mark.parametrize("tile", [22, 23, 24, 25, 29, 30, 31, 32, 38, 39])
 def test_conv_bf16x6_se_scale(tile):
     _conv_case(2, 10, 10, 480, 160, 1, 1, None, True, tile=tile, se=True, x6=True)
 

@@ -27,11 +27,23 @@ if [ "${BENCH:-1}" = "1" ]; then
   step bench_driver 900 python -u bench.py --gpus 1 --steps 20 --warmup 5
 fi
 if [ "${AB:-1}" = "1" ]; then
+  # ABBA order (alternated pairs showed the first run of each pair ~1% high whatever its variant)
   for r in 1 2; do
-    for v in 1 0; do EDGEDET_STEM_MFMA=$v step ab_stem${v}_r$r 300 python -u $SSD_AB; done
+    o="1 0"; [ $r = 2 ] && o="0 1"
+    for v in $o; do EDGEDET_STEM_MFMA=$v step ab_stem${v}_r$r 300 python -u $SSD_AB; done
   done
   for r in 1 2; do
-    for t in 29 31; do EDGEDET_HEAD_TILE=$t step ab_tile${t}_r$r 300 python -u $SSD_AB; done
+    o="29 31"; [ $r = 2 ] && o="31 29"
+    for t in $o; do EDGEDET_HEAD_TILE=$t step ab_tile${t}_r$r 300 python -u $SSD_AB; done
+  done
+fi
+if [ "${FAB:-0}" = "1" ]; then  # FRCNN: the Cout = 256 layers (and the RPN head groups) on the 128 x 256 tile
+  step pytest_t39 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k bf16x6 --timeout 120 --timeout-method thread
+  step conv39 300 python -u tools/conv_bench.py --tiles 25,39 --shapes box_head_3x3,fpn_p2_3x3,layer3_3x3 --reps 20
+  FRCNN_AB="bench.py --model frcnn --steps 200 --warmup 10 --no-cpu --no-e2e --no-roofline --no-alt"
+  for r in 1 2; do
+    step ab_t39_0_r$r 300 python -u $FRCNN_AB
+    EDGEDET_TILE39=1 EDGEDET_RPN_TILE=39 step ab_t39_1_r$r 300 python -u $FRCNN_AB
   done
 fi
 if [ "${LONG:-1}" = "1" ]; then
