@@ -23,6 +23,7 @@ import torch
 
 from . import arch
 from . import native
+from . import ops
 from .plan import NativePlan
 
 
@@ -315,7 +316,7 @@ class SSDLite320(_Detector):
         """Named buffers of the SSDLite plan the parity tests read (csrc/lower.hip SSDLite)."""
         P.cls_logits, P.bbox_regression = P.buffer("cls_logits"), P.buffer("bbox_regression")
         P.scores_t, P.boxes = P.buffer("scores_t"), P.buffer("boxes")
-        P.chains = max(1, sum(1 for n in P.buffers if n.startswith("backbone.features.0.13#")))
+        P.chains = 1 + next((int(r["i"][0]) for r in P.records if int(r["kind"]) == ops.FORK), 0)  # side lanes + 1
 
 
 # ====================================================================================== FRCNN

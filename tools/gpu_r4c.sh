@@ -46,6 +46,13 @@ if [ "${FAB:-0}" = "1" ]; then  # FRCNN: the Cout = 256 layers (and the RPN head
     EDGEDET_TILE39=1 EDGEDET_RPN_TILE=39 step ab_t39_1_r$r 300 python -u $FRCNN_AB
   done
 fi
+if [ "${MERGE:-0}" = "1" ]; then  # SSD: chains merged after block features.0.<m> (0: never)
+  step pytest_merge 300 python -u -m pytest tests/test_gpu_models.py -q -x -k chains_agree -s --timeout 200 --timeout-method thread
+  for r in 1 2; do
+    o="${MERGES:-0 3 5 7 9 12}"; [ $r = 2 ] && o=$(echo $o | tr ' ' '\n' | tac | tr '\n' ' ')
+    for m in $o; do EDGEDET_SSD_MERGE=$m step ab_merge${m}_r$r 300 python -u $SSD_AB; done
+  done
+fi
 if [ "${LONG:-1}" = "1" ]; then
   step bench_long 600 python -u bench.py --model both --steps 750 --warmup 20 --no-cpu --no-e2e --dump-ops gpurun_out/ops_long.json
 fi
