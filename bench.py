@@ -140,6 +140,12 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     el = mark.elapsed_time(done[-1]) / 1e3 * steps / (steps + r)
+    if os.environ.get("EDGEDET_BENCH_TRACE"):  # per-pass completion times (timing investigation)
+        with open(os.environ["EDGEDET_BENCH_TRACE"], "a") as fh:
+            fh.write(json.dumps({"n": n, "r": r, "warm": warm, "settled": settled,
+                                 "streams": [int(s_.cuda_stream) for _, s_, _ in lanes],
+                                 "pass_lane": [(settled + warm + i) % n for i in range(steps)],
+                                 "done_ms": [round(mark.elapsed_time(e), 3) for e in done]}) + "\n")
     if dist:
         dist.barrier()
         t = torch.tensor([el, wall], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")

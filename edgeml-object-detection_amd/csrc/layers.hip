@@ -324,12 +324,15 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
 // 16 + BN + ReLU, projection 1x1 16 -> 16 + BN, + the stem output) in one pass: the two 16-channel
 // 160x160 tensors between them never reach HBM.  Block = one image, a 16 x 16 output tile:
 //   1. the 37 x 37 x 4 input tile (stride-2 receptive field of the 18 x 18 stem halo) into LDS;
-//   2. stem outputs on the 18 x 18 halo (zero outside the map: the depthwise pads them), one pixel x
-//      16 channels per thread, taps in the packed (kh, kw, ci) order;
-//   3. per output pixel: depthwise (taps (kh, kw) as dw_group), projection, + bias, + residual.
-// The weights (1024 floats) are staged in LDS with the input tile, in the same memory round trip, and
-// read as wave-wide broadcasts (as scalar loads they did not fit the SGPRs and were re-fetched per
-// pixel: the kernel waited on the scalar cache for half its lifetime).
+//   2. stem outputs on the 18 x 18 halo (zero outside the map: the depthwise pads them) as a GEMM on
+//      the matrix cores, [324 halo pixels] x [36 = 9 taps x 4 channels] x [16], one
+//      v_mfma_f32_16x16x4_f32 per tap (exact fp32 products);
+//   3. per output pixel: depthwise on the vector ALUs (taps (kh, kw) as dw_group), then the projection
+//      as a [256 pixels] x [16] x [16] MFMA GEMM, + bias, + residual.
+// The matrix-core form replaced one pixel x 16 channels per thread on the vector ALUs for phases 2 and
+// 3 (SSD 30.63k / 30.63k -> 30.87k / 30.95k img/s in ABBA-ordered runs, profiles/r4c_ab.txt).  The
+// weights (1024 floats) are staged in LDS with the input tile, in the same memory round trip (as
+// scalar loads they did not fit the SGPRs and were re-fetched per pixel).
 constexpr int STEM_T = 16, STEM_SH = STEM_T + 2, STEM_XH = 2 * STEM_SH + 1, STEM_SS = 20;
 // LDS weight image: w0 [16][36] (taps (kh, kw, ci)), b0 [16], wd [9][16], bd [16], w1 [16][16], b1 [16]
 constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 = 752, STEM_B1 = 1008, STEM_NW = 1024;
@@ -337,7 +340,7 @@ constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 
 // T = float: the transform's NHWC4 output (p.x); T = float / uint8_t with FUSED: the source image
 // (p.src / p.src8, [B][3][H0][W0]) and the transform computed per input pixel of the tile (pre_pixel,
 // the same bits as the transform kernel): no transform launch and no NHWC4 round trip through HBM.
-template <typename T, bool FUSED, bool MF>
+template <typename T, bool FUSED>
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
@@ -385,114 +388,45 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
     }
     __syncthreads();
     const int lane = tid & 63, wid = tid >> 6, l16 = lane & 15, q4 = lane >> 4;
-    if constexpr (MF) {
-        // stem conv as a GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32 products): rows =
-        // the 324 halo pixels in 21 tiles of 16 (wave w takes tiles w, w + 4, ...), columns = the 16
-        // output channels, K = 9 taps x 4 channels in the packed (kh, kw, ci) order (one MFMA per tap)
-        float wb[9];
+    // stem conv as a GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32 products): rows =
+    // the 324 halo pixels in 21 tiles of 16 (wave w takes tiles w, w + 4, ...), columns = the 16
+    // output channels, K = 9 taps x 4 channels in the packed (kh, kw, ci) order (one MFMA per tap)
+    float wb[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) wb[t] = ws[STEM_W0 + l16 * 36 + 4 * t + q4];
-        const float b0v = ws[STEM_B0 + l16];
-        constexpr int NV = STEM_SH * STEM_SH, NTL = (NV + 15) / 16;
-        for (int tl = wid; tl < NTL; tl += 4) {
-            const int va = min(16 * tl + l16, NV - 1);  // this lane's A row (pad rows repeat the last pixel)
-            const int lh = va / STEM_SH, lw = va - lh * STEM_SH;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 9; ++t) wb[t] = ws[STEM_W0 + l16 * 36 + 4 * t + q4];
+    const float b0v = ws[STEM_B0 + l16];
+    constexpr int NV = STEM_SH * STEM_SH, NTL = (NV + 15) / 16;
+    for (int tl = wid; tl < NTL; tl += 4) {
+        const int va = min(16 * tl + l16, NV - 1);  // this lane's A row (pad rows repeat the last pixel)
+        const int lh = va / STEM_SH, lw = va - lh * STEM_SH;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const float av = xs[4 * ((2 * lh + t / 3) * STEM_XH + 2 * lw + t % 3) + q4];
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[t], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int v = 16 * tl + 4 * q4 + i;
-                if (v < NV) {
-                    const int vh = v / STEM_SH, vw = v - vh * STEM_SH;
-                    const bool in = (unsigned)(sh0 + vh) < (unsigned)p.Ho && (unsigned)(sw0 + vw) < (unsigned)p.Wo;
-                    ss[v * STEM_SS + l16] = in ? apply_act(acc[i] + b0v, ACT_HSWISH) : 0.f;
-                }
-            }
+        for (int t = 0; t < 9; ++t) {
+            const float av = xs[4 * ((2 * lh + t / 3) * STEM_XH + 2 * lw + t % 3) + q4];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[t], acc, 0, 0, 0);
         }
-    } else
-    for (int v = tid; v < STEM_SH * STEM_SH; v += 256) {
-        asm volatile("" ::: "memory");  // keep the weight reads in the loop (hoisted, they took 256 VGPRs)
-        const int lh = v / STEM_SH, lw = v % STEM_SH;
-        const bool in = (unsigned)(sh0 + lh) < (unsigned)p.Ho && (unsigned)(sw0 + lw) < (unsigned)p.Wo;
-        f32x4 xt[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
-            xt[t] = *reinterpret_cast<const f32x4*>(xs + 4 * ((2 * lh + t / 3) * STEM_XH + 2 * lw + t % 3));
-        float* d = ss + v * STEM_SS;
-#pragma unroll
-        for (int co = 0; co < 16; ++co) {
-            const float* w = ws + STEM_W0 + co * 36;
-            float acc = 0.f;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                acc = fmaf(w[4 * t + 0], xt[t].x, acc);
-                acc = fmaf(w[4 * t + 1], xt[t].y, acc);
-                acc = fmaf(w[4 * t + 2], xt[t].z, acc);
-                acc = fmaf(w[4 * t + 3], xt[t].w, acc);
+        for (int i = 0; i < 4; ++i) {
+            const int v = 16 * tl + 4 * q4 + i;
+            if (v < NV) {
+                const int vh = v / STEM_SH, vw = v - vh * STEM_SH;
+                const bool in = (unsigned)(sh0 + vh) < (unsigned)p.Ho && (unsigned)(sw0 + vw) < (unsigned)p.Wo;
+                ss[v * STEM_SS + l16] = in ? apply_act(acc[i] + b0v, ACT_HSWISH) : 0.f;
             }
-            d[co] = in ? apply_act(acc + ws[STEM_B0 + co], ACT_HSWISH) : 0.f;
         }
     }
     __syncthreads();
     const int lh = tid / STEM_T, lw = tid % STEM_T;
     const int oh = oh0 + lh, ow = ow0 + lw;
-    if constexpr (MF) {
-        // depthwise on the vector ALUs (one output pixel x 16 channels per thread, taps (kh, kw)), its
-        // outputs through LDS (the input tile's space, free now) into the projection GEMM on the matrix
-        // cores: rows = the wave's 64 pixels in 4 tiles, columns = 16 channels, K = 16 in 4 steps
-        float dv[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) dv[c] = 0.f;
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-            if ((unsigned)(oh - 1 + kh) >= (unsigned)p.Ho) continue;
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const float* sv = ss + ((lh + kh) * STEM_SH + lw + kw) * STEM_SS;
-                const float* wv = ws + STEM_WD + (kh * 3 + kw) * 16;
-#pragma unroll
-                for (int c = 0; c < 16; ++c) dv[c] = fmaf(sv[c], wv[c], dv[c]);
-            }
-        }
-        constexpr int DS = 17;  // odd pitch
-        float* dsm = xs;        // [256][DS]
-#pragma unroll
-        for (int c = 0; c < 16; ++c) dsm[tid * DS + c] = apply_act(dv[c] + ws[STEM_BD + c], ACT_RELU);
-        float w1v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w1v[k] = ws[STEM_W1 + l16 * 16 + 4 * k + q4];
-        const float b1v = ws[STEM_B1 + l16];
-        __syncthreads();
-#pragma unroll
-        for (int tl = 0; tl < 4; ++tl) {
-            const int row0 = 64 * wid + 16 * tl;  // the tile's first output pixel (= thread index)
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dsm[(row0 + l16) * DS + 4 * k + q4], w1v[k], acc, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int px = row0 + 4 * q4 + i, ph = px / STEM_T, pw = px % STEM_T;
-                const int yh = oh0 + ph, yw = ow0 + pw;
-                if (yh < p.Ho && yw < p.Wo) {
-                    const float r = ss[((ph + 1) * STEM_SH + pw + 1) * STEM_SS + l16];
-                    p.y[(((int64_t)b * p.Ho + yh) * p.Wo + yw) * 16 + l16] = (acc[i] + b1v) + r;
-                }
-            }
-        }
-        return;
-    }
-    if (oh >= p.Ho || ow >= p.Wo) return;
+    // depthwise on the vector ALUs (one output pixel x 16 channels per thread, taps (kh, kw)), its
+    // outputs through LDS (the input tile's space, free now) into the projection GEMM on the matrix
+    // cores: rows = the wave's 64 pixels in 4 tiles, columns = 16 channels, K = 16 in 4 steps
     float dv[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) dv[c] = 0.f;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
-        if ((unsigned)(oh - 1 + kh) >= (unsigned)p.Ho) continue;  // dw_group skips rows outside the map
+        if ((unsigned)(oh - 1 + kh) >= (unsigned)p.Ho) continue;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
             const float* sv = ss + ((lh + kh) * STEM_SH + lw + kw) * STEM_SS;
@@ -501,22 +435,32 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             for (int c = 0; c < 16; ++c) dv[c] = fmaf(sv[c], wv[c], dv[c]);
         }
     }
+    constexpr int DS = 17;  // odd pitch
+    float* dsm = xs;        // [256][DS]
 #pragma unroll
-    for (int c = 0; c < 16; ++c) dv[c] = apply_act(dv[c] + ws[STEM_BD + c], ACT_RELU);
-    const float* res = ss + ((lh + 1) * STEM_SH + lw + 1) * STEM_SS;
-    float out[16];
+    for (int c = 0; c < 16; ++c) dsm[tid * DS + c] = apply_act(dv[c] + ws[STEM_BD + c], ACT_RELU);
+    float w1v[4];
 #pragma unroll
-    for (int co = 0; co < 16; ++co) {
-        const float* w = ws + STEM_W1 + co * 16;
-        float acc = 0.f;
+    for (int k = 0; k < 4; ++k) w1v[k] = ws[STEM_W1 + l16 * 16 + 4 * k + q4];
+    const float b1v = ws[STEM_B1 + l16];
+    __syncthreads();
 #pragma unroll
-        for (int ci = 0; ci < 16; ++ci) acc = fmaf(w[ci], dv[ci], acc);
-        out[co] = (acc + ws[STEM_B1 + co]) + res[co];
+    for (int tl = 0; tl < 4; ++tl) {
+        const int row0 = 64 * wid + 16 * tl;  // the tile's first output pixel (= thread index)
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dsm[(row0 + l16) * DS + 4 * k + q4], w1v[k], acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int px = row0 + 4 * q4 + i, ph = px / STEM_T, pw = px % STEM_T;
+            const int yh = oh0 + ph, yw = ow0 + pw;
+            if (yh < p.Ho && yw < p.Wo) {
+                const float r = ss[((ph + 1) * STEM_SH + pw + 1) * STEM_SS + l16];
+                p.y[(((int64_t)b * p.Ho + yh) * p.Wo + yw) * 16 + l16] = (acc[i] + b1v) + r;
+            }
+        }
     }
-    float* yp = p.y + (((int64_t)b * p.Ho + oh) * p.Wo + ow) * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<f32x4*>(yp + 4 * q) = f32x4{out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
 }
 
 int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
@@ -533,15 +477,8 @@ int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
     EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
     const int tiles_w = cdiv(p.Wo, STEM_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B);
-    // the matrix-core form (stem conv and projection on v_mfma_f32_16x16x4_f32); EDGEDET_STEM_MFMA=0
-    // keeps the vector-ALU form (temporary A/B switch, round 4)
-    static const bool mf = [] {
-        const char* e = std::getenv("EDGEDET_STEM_MFMA");
-        return !(e && e[0] == '0');
-    }();
-    void (*k)(StemParams, int) = p.src8 ? (mf ? ssd_stem_kernel<uint8_t, true, true> : ssd_stem_kernel<uint8_t, true, false>)
-                                 : p.src ? (mf ? ssd_stem_kernel<float, true, true> : ssd_stem_kernel<float, true, false>)
-                                         : (mf ? ssd_stem_kernel<float, false, true> : ssd_stem_kernel<float, false, false>);
+    void (*k)(StemParams, int) = p.src8 ? ssd_stem_kernel<uint8_t, true>
+                                 : p.src ? ssd_stem_kernel<float, true> : ssd_stem_kernel<float, false>;
     hipLaunchKernelGGL(k, grid, dim3(256), 0, s, p, tiles_w);
     EDGEDET_LAUNCH_CHECK();
     return 0;

@@ -469,8 +469,12 @@ static void conv_op(Plan& P, const ConvArgs& a) {
         auto it = tile_table().find(conv_key(o));
         if (it != tile_table().end() && it->second && (w3 || it->second < 20)) o.i[23] = it->second;
     }
-    // temporary A/B switch (round 4): the Cout = 256 layers of tile 25 on the 128 x 256 tile
-    if (o.i[23] == 25 && a.cout == 256 && env_int("EDGEDET_TILE39", 0) == 1) o.i[23] = 39;
+    // the Cout = 256 layers the table puts on 256 x 128 run the 128 x 256 tile: one N tile, so each A
+    // panel is read once (FRCNN 362.6 / 362.5 -> 369.9 / 373.8 img/s in alternated runs; box head 3x3
+    // 2.09 -> 1.88 ms in the conv microbench, profiles/r4c_conv39.txt); input-transformed layers keep
+    // 25 and its pre-split input (below)
+    const bool xf = a.in_scale.kind != Ref::NONE || a.in_shift.kind != Ref::NONE || a.in_relu;
+    if (o.i[23] == 25 && a.cout == 256 && !xf) o.i[23] = 39;
     if (o.i[23] == 26) {
         const bool dense = yp == a.cout && a.y_off == 0 && (a.y_bstride < 0 || a.y_bstride == Ho * Wo * a.cout);
         if (a.act == 0 && a.res.kind == Ref::NONE && dense && w3) {
@@ -484,7 +488,6 @@ static void conv_op(Plan& P, const ConvArgs& a) {
             o.i[23] = 25;
         }
     }
-    const bool xf = a.in_scale.kind != Ref::NONE || a.in_shift.kind != Ref::NONE || a.in_relu;
     // pre-split input planes only where an input transform is fused (GN / SE / ReLU on load): the split
     // pass then also takes the per-element transform out of the GEMM loop; for a plain input the extra
     // HBM pass measured slower (FRCNN 336 -> 313 img/s)
@@ -599,25 +602,15 @@ class SSDLite {
         int nch = pack_only ? 1 : n_chains(B);
         const int inp = P->buf({B, 3, H, W}, u8 ? 1 : 4, "images");
         Shared sh;
-        // the chains run the early layers (stem .. block features.0.<m-1>) on their own batch slices, then
-        // join, and the rest of the network runs once over the whole batch (EDGEDET_SSD_MERGE = m in
-        // 2..12; 0: the chains run to the end)
-        const int m = nch > 1 ? std::max(0, std::min(12, env_int("EDGEDET_SSD_MERGE", 0))) : 0;
-        sh.merge = m >= 2;
-        const int to = sh.merge ? m : END;
         if (nch > 1) P->fork(nch - 1);
         const int q = B / nch, r = B % nch;
         for (int c = 0; c < nch; ++c) {
             const int b0 = c * q + std::min(c, r), bc = q + (c < r ? 1 : 0);
             if (nch > 1) P->lane(c);
-            chain(*P, c, b0, bc, B, H, W, u8, inp, sh, nch, pack_only, 0, to, nullptr);
+            chain(*P, c, b0, bc, B, H, W, u8, inp, sh, nch, pack_only);
             if (pack_only) return P;
         }
         if (nch > 1) P->join();
-        if (sh.merge) {
-            const Cur st{P->ref(sh.last), P->bufs[(size_t)sh.last].shape};
-            chain(*P, 0, 0, B, B, H, W, u8, inp, sh, 1, false, m, END, &st);
-        }
         P->input = inp;
         P->out_box = sh.ob;
         P->out_score = sh.os;
@@ -631,11 +624,7 @@ class SSDLite {
     struct Shared {
         int cls = -1, reg = -1, anchors = -1, scores_t = -1, boxes = -1, ratio = -1, ob = -1, os = -1, ol = -1,
             oc = -1;
-        bool merge = false;              // activations in whole-batch buffers, the chains on slices
-        std::map<std::string, int> acts;  // activation name -> whole-batch buffer
-        int last = -1;                   // the last activation buffer handed out
     };
-    static constexpr int END = 1 << 20;  // chain(): run to the end of the network
 
     int n_chains(int B) const {
         const int n = env_int("EDGEDET_SSD_CHAINS", 0) ? env_int("EDGEDET_SSD_CHAINS", 0) : 2;
@@ -646,26 +635,11 @@ class SSDLite {
         return pk_.conv_bn(prefix + ".0.weight", prefix + ".1", EPS, cout, cin, k, dw, cin_pad);
     }
 
-    // One chain of the forward over images [img0, img0 + B) of the Btot-image batch: from block
-    // features.0.<from> (0: the transform + stem; `start` is then null, else the input activation) up to
-    // block features.0.<to> (END: through the heads and the post-process).
     void chain(Plan& P, int c, int img0, int B, int Btot, int H, int W, bool u8, int inp, Shared& sh, int nch,
-               bool pack_only, int from, int to, const Cur* start) {
+               bool pack_only) {
         const int NC = cfg_.num_classes;
         const std::string sfx = nch > 1 ? "#" + std::to_string(c) : "";
         auto view = [&](int b) { return nch > 1 ? P.view(b, img0) : P.ref(b); };
-        // an activation buffer: the chain's own, or (merged plans) its slice of a whole-batch buffer
-        auto act = [&](const std::vector<int64_t>& ys, const std::string& name) {
-            if (!sh.merge) return P.ref(P.buf(ys, 4, name + sfx));
-            auto it = sh.acts.find(name);
-            if (it == sh.acts.end()) {
-                std::vector<int64_t> s = ys;
-                s[0] = Btot;
-                it = sh.acts.emplace(name, P.buf(s, 4, name)).first;
-            }
-            sh.last = it->second;
-            return view(it->second);
-        };
         // the transform (normalise 0.5 / 0.5, resize to S x S): folded into the fused stem's input loads
         // (EDGEDET_SSD_STEM_FUSE=1, the default), else its own record into an NHWC4 buffer
         const bool stem_fuse = env_int("EDGEDET_SSD_STEM_FUSE", 1) == 1 && !pack_only;
@@ -684,13 +658,13 @@ class SSDLite {
             cur = Cur{P.ref(x), {B, S, S, 4}};
         }
 
-        auto conv = [&](const Cur& in, const std::string& prefix, int64_t cout, int k, int stride, int actf,
+        auto conv = [&](const Cur& in, const std::string& prefix, int64_t cout, int k, int stride, int act,
                         Ref res = Ref(), Ref in_scale = Ref(), int64_t cin_pad = 0) {
             ConvW w = cbn(prefix, cout, cin_pad ? 3 : in.s[3], k, false, cin_pad);
             const int pad = (k - 1) / 2;
             const int64_t Ho = (in.s[1] + 2 * pad - k) / stride + 1, Wo = (in.s[2] + 2 * pad - k) / stride + 1;
             std::vector<int64_t> ys = {B, Ho, Wo, cout};
-            const Ref y = act(ys, prefix);
+            const int y = P.buf(ys, 4, prefix + sfx);
             ConvArgs a;
             a.x = in.x;
             a.xs = in.s;
@@ -699,41 +673,41 @@ class SSDLite {
             a.k = k;
             a.stride = stride;
             a.pad = pad;
-            a.act = actf;
-            a.y = y;
+            a.act = act;
+            a.y = P.ref(y);
             a.ys = ys;
             a.res = res;
             a.in_scale = in_scale;
             a.name = prefix;
             conv_op(P, a);
-            return Cur{y, ys};
+            return Cur{P.ref(y), ys};
         };
         struct DwOut {
             Cur y;
             int part = -1, parts = 0;
         };
-        auto dw = [&](const Cur& in, const std::string& prefix, int k, int stride, int actf, bool se_part) {
+        auto dw = [&](const Cur& in, const std::string& prefix, int k, int stride, int act, bool se_part) {
             const int64_t C = in.s[3];
             ConvW w = cbn(prefix, C, C, k, true);
             const int pad = (k - 1) / 2;
             const int64_t Ho = (in.s[1] + 2 * pad - k) / stride + 1, Wo = (in.s[2] + 2 * pad - k) / stride + 1;
             std::vector<int64_t> ys = {B, Ho, Wo, C};
-            const Ref y = act(ys, prefix);
+            const int y = P.buf(ys, 4, prefix + sfx);
             const int64_t groups = Ho * ((Wo + 3) / 4);
             const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(SE_PARTS, groups / 16));
             const int part = se_part ? P.buf({B, parts, C}, 4, prefix + ".se_partial_sums" + sfx) : -1;
             OpRec o;
             o.kind = EDGEDET_OP_DWCONV;
             o.name = prefix;
-            const int64_t iv[11] = {B, in.s[1], in.s[2], C, Ho, Wo, k, stride, pad, actf, parts};
+            const int64_t iv[11] = {B, in.s[1], in.s[2], C, Ho, Wo, k, stride, pad, act, parts};
             for (int j = 0; j < 11; ++j) o.i[j] = iv[j];
             o.p[0] = in.x;
             o.p[1] = Plan::wref(w.w);
             o.p[2] = Plan::wref(w.b);
-            o.p[3] = y;
+            o.p[3] = P.ref(y);
             o.p[4] = part >= 0 ? P.ref(part) : Ref();
             P.add(o);
-            return DwOut{Cur{y, ys}, part, parts};
+            return DwOut{Cur{P.ref(y), ys}, part, parts};
         };
         auto se = [&](const DwOut& in, const std::string& p) {
             const int64_t C = in.y.s[3];
@@ -764,7 +738,7 @@ class SSDLite {
             const int pad = (b.k - 1) / 2;
             const int64_t Ho = (in.s[1] + 2 * pad - b.k) / b.stride + 1, Wo = (in.s[2] + 2 * pad - b.k) / b.stride + 1;
             std::vector<int64_t> ys = {B, Ho, Wo, b.cout};
-            const Ref y = act(ys, pf.pp);
+            const int y = P.buf(ys, 4, pf.pp + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_MBCONV;
             o.name = pf.pe.substr(0, pf.pe.rfind('.'));
@@ -778,9 +752,9 @@ class SSDLite {
             o.p[4] = Plan::wref(wd.b);
             o.p[5] = Plan::wref(w2.w);
             o.p[6] = Plan::wref(w2.b);
-            o.p[7] = y;
+            o.p[7] = P.ref(y);
             P.add(o);
-            return Cur{y, ys};
+            return Cur{P.ref(y), ys};
         };
         auto inverted_residual = [&](const Cur& in, const Block& b, const std::string& base) {
             Prefixes pf = block_prefixes(b, base);
@@ -798,17 +772,14 @@ class SSDLite {
         };
 
         int first = 0;
-        if (from > 0) {
-            cur = *start;
-            first = from;
-        } else if (stem_fuse) {
+        if (stem_fuse) {
             ConvW w0 = cbn("backbone.features.0.0", 16, 3, 3, false, 4);
             Prefixes pf = block_prefixes(blocks_[0], "backbone.features.0.1.block");
             ConvW wd = cbn(pf.pd, 16, 16, 3, true);
             ConvW w1 = cbn(pf.pp, 16, 16, 1, false);
             const int64_t Ho = (S - 1) / 2 + 1, Wo = Ho;
             std::vector<int64_t> ys = {B, Ho, Wo, 16};
-            const Ref y = act(ys, "backbone.features.0.1");
+            const int y = P.buf(ys, 4, "backbone.features.0.1" + sfx);
             OpRec o;
             o.kind = EDGEDET_OP_SSD_STEM;
             o.name = "transform+backbone.features.0.0+0.1";
@@ -822,16 +793,15 @@ class SSDLite {
             o.p[4] = Plan::wref(wd.b);
             o.p[5] = Plan::wref(w1.w);
             o.p[6] = Plan::wref(w1.b);
-            o.p[7] = y;
+            o.p[7] = P.ref(y);
             P.add(o);
-            cur = Cur{y, ys};
+            cur = Cur{P.ref(y), ys};
             first = 1;
         } else {
             cur = conv(cur, "backbone.features.0.0", 16, 3, 2, A_HS, Ref(), Ref(), 4);
         }
-        for (int i = first; i < std::min(12, to); ++i)
+        for (int i = first; i < 12; ++i)
             cur = inverted_residual(cur, blocks_[(size_t)i], "backbone.features.0." + std::to_string(i + 1) + ".block");
-        if (to != END) return;  // the merge point: the rest runs over the whole batch
         const Block& b12 = blocks_[12];
         cur = conv(cur, "backbone.features.0.13", b12.exp, 1, 1, b12.act);
         std::vector<Cur> feats = {cur};
@@ -914,7 +884,7 @@ class SSDLite {
             a.y_pstride = 6 * h.cols;
             a.y_bstride = A * h.cols;
             a.y_off = (int64_t)img0 * A * h.cols + h.off * h.cols;
-            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") ? 0 : env_int("EDGEDET_HEAD_TILE", HEAD_TILE);  // f32: alone
+            a.tile = env_is("EDGEDET_CONV_MATH", "f32", "bf16x6") ? 0 : HEAD_TILE;  // f32: alone
             a.name = h.p + ".1" + sfx;
             conv_op(P, a);
         }
@@ -1251,7 +1221,7 @@ static std::vector<float> grid_anchors(int gh, int gw, int Hp, int Wp, const std
 class FasterRCNN : public ResNetFPN {
   public:
     static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
-    static constexpr int RPN_TILE = 25;
+    static constexpr int RPN_TILE = 39;  // the grouped RPN head 3x3 convs (Cout = 256): 128 x 256
     static constexpr int RPN_CHUNK = 8192;  // anchors per chunk of the chunked RPN top-k  // the grouped RPN 3x3 convs: the P2 level's tuned tile (256 x 128)
     static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
                             BOX_MIN = 1e-2;
@@ -1317,7 +1287,7 @@ class FasterRCNN : public ResNetFPN {
             COpt o;
             o.bias_key = "rpn.head.conv.0.0.bias";
             o.name = "rpn.head.conv.0@" + std::to_string(lvl);
-            o.tile = grouped ? env_int("EDGEDET_RPN_TILE", RPN_TILE) : 0;
+            o.tile = grouped ? RPN_TILE : 0;
             t0s.push_back(conv(P, outs[(size_t)lvl], "rpn.head.conv.0.0.weight", 256, 3, 1, A_RE, o));
         }
         if (grouped) rpn_group("rpn.head.conv.1");
@@ -1325,7 +1295,7 @@ class FasterRCNN : public ResNetFPN {
             COpt o;
             o.bias_key = "rpn.head.conv.1.0.bias";
             o.name = "rpn.head.conv.1@" + std::to_string(lvl);
-            o.tile = grouped ? env_int("EDGEDET_RPN_TILE", RPN_TILE) : 0;
+            o.tile = grouped ? RPN_TILE : 0;
             t1s.push_back(conv(P, t0s[(size_t)lvl], "rpn.head.conv.1.0.weight", 256, 3, 1, A_RE, o));
         }
         for (int lvl = 0; lvl < L5; ++lvl) {
