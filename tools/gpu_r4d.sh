@@ -24,4 +24,7 @@ rm -f gpurun_out/trace_*.jsonl
 EDGEDET_BENCH_TRACE=gpurun_out/trace_frcnn.jsonl step tr_frcnn 300 python -u bench.py --model frcnn --steps 200 --warmup 10 --no-cpu --no-e2e --no-roofline --no-alt
 EDGEDET_BENCH_TRACE=gpurun_out/trace_both.jsonl step tr_both 300 python -u bench.py --model both --steps 200 --warmup 10 --no-cpu --no-e2e --no-roofline --no-alt
 step bench_driver 900 python -u bench.py --gpus 1 --steps 20 --warmup 5
+if [ "${STAGE:-1}" = "1" ]; then
+  step stage_error 600 python -u tools/stage_error.py --images 0,1,2 -o gpurun_out/stage_error.json
+fi
 exit 0
