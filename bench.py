@@ -86,18 +86,22 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
 
     Steady state (round 4): a completion event is recorded on the instance's stream after each pass's
     D2H.  The pipeline is NOT drained between the warmup and the timed passes, so the timed region
-    starts full, as in a long run, with no fill or drain latency in the denominator.  The interval
-    runs between two completions of the SAME instance: from a warmup pass j0 to the last timed pass,
-    j0 chosen r = (-K) mod n passes before the last warmup pass so that K + r is a multiple of the n
-    instances.  Concurrent instances can finish in bursts (three FRCNN plans sharing the chip finish
-    close together), and an interval that starts at the first completion of a burst counts the rest
-    of that burst for free: with K = 20 and n = 3 that read 443 FRCNN img/s against 340 in a long run
-    (profiles/r4c_bench_driver_bias.json).  Between two completions of one instance the pipeline is
-    in the same phase, so the interval holds exactly (K + r) / n cycles; the time returned is that
-    interval scaled by K / (K + r).  Every instance was primed when it was captured (graph uploaded
-    and replayed, plan.capture), and the warmup covers each instance at least once.  The ranks start
-    together (barrier + device sync before the warmup) and end together (device sync + barrier after
-    the last pass); the max over ranks is taken.  The host wall clock of the K timed passes (from the
+    starts full, as in a long run, with no fill or drain latency in the denominator; the host keeps at
+    most 2n passes outstanding throughout (settle, warmup and timed passes alike).  The interval runs
+    between two completions of the SAME instance: from a warmup pass j0 to the last timed pass, j0
+    chosen r = (-K) mod n passes before the last warmup pass so that K + r is a multiple of the n
+    instances; between two completions of one instance the pipeline is in the same phase, so the
+    interval holds (K + r) / n cycles, and the time returned is that interval scaled by K / (K + r).
+    Concurrent instances can finish in bursts (the three FRCNN plans finish within a few ms of each
+    other every ~68 ms, profiles/r4d_trace_frcnn.jsonl), so an interval between completions of
+    different instances would count part of a burst for free.  Two earlier forms read too high on
+    FRCNN after the SSD run (443 and 538 img/s against ~360, profiles/r4c_bench_driver_bias.json): the
+    timed passes were issued all at once, and two of the three instances' streams shared a hardware
+    queue, so the third instance ran ahead alone inside the window (profiles/r4d_trace_both.jsonl);
+    the issue discipline and fresh per-model streams (main) remove both.  Every instance was primed
+    when it was captured (graph uploaded and replayed, plan.capture), and the warmup covers each
+    instance at least once.  The ranks start together (barrier + device sync before the warmup) and
+    end together (device sync + barrier after the last pass); the max over ranks is taken.  The host wall clock of the K timed passes (from the
     first timed issue to the final sync, so it includes the drain) is kept in TIMING."""
     lanes = [(p, s, d2h_buffers(p)) for p, s in [(plan, stream)] + list(extra)]
     n = len(lanes)
@@ -109,32 +113,35 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     # (round robin, never drained: the host waits only for the pass 2n back, so the instances keep the
     # staggered phases of a long run instead of starting in lockstep) -- the clocks and the overlap the
     # timed passes see are a long run's (profiles/r4a_bench_driver.json: 1.67 ms/step over 20 steps
-    # right after an idle host phase, against 1.38 in a 750-step run)
-    t_settle, settled, ring = time.perf_counter(), 0, []
-    while time.perf_counter() - t_settle < SETTLE_S or settled < 2 * n:
-        p_, s_, d_ = lanes[settled % n]
+    # right after an idle host phase, against 1.38 in a 750-step run).  Settle, warmup and timed
+    # passes share one issue discipline (issue): at most 2n passes outstanding.  Issued all at once,
+    # an instance whose stream had no backlog ran ahead of the others inside the timed window and the
+    # interval measured it alone (profiles/r4d_trace_both.jsonl).
+    ring = []  # completion events of the outstanding passes, oldest first
+
+    def issue(k, timing=False):  # pass k round robin; at most 2n passes outstanding before it
+        while len(ring) >= 2 * n:
+            ring.pop(0).synchronize()
+        p_, s_, d_ = lanes[k % n]
         step(p_, s_, d_)
-        e = torch.cuda.Event()
+        e = torch.cuda.Event(enable_timing=timing)
         e.record(s_)
         ring.append(e)
-        if len(ring) > 2 * n:
-            ring.pop(0).synchronize()
+        return e
+
+    t_settle, settled = time.perf_counter(), 0
+    while time.perf_counter() - t_settle < SETTLE_S or settled < 2 * n:
+        issue(settled)
         settled += 1
     r = (-steps) % n  # warm >= n > r: the interval's first completion is a warmup pass
     for i in range(warm):
-        p_, s_, d_ = lanes[(settled + i) % n]
-        step(p_, s_, d_)
+        e = issue(settled + i, timing=i == warm - 1 - r)
         if i == warm - 1 - r:
-            mark = torch.cuda.Event(enable_timing=True)
-            mark.record(s_)
+            mark = e
     done = []
     t0 = time.perf_counter()
     for i in range(steps):
-        p, s, d2h = lanes[(settled + warm + i) % n]
-        step(p, s, d2h)
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(s)
-        done.append(e)
+        done.append(issue(settled + warm + i, timing=True))
     for _, s, _ in lanes:
         s.synchronize()
     torch.cuda.synchronize()
@@ -225,6 +232,7 @@ CONV_TILES = {  # tile id (csrc/conv.hip conv_launch) -> kernel, BM, BN, threads
     25: ("conv_x6b_kernel", 256, 128, 512), 27: ("conv_x6_kernel", 128, 64, 512), 28: ("conv_x6_kernel", 128, 128, 512),
     29: ("conv_x6b_kernel", 128, 128, 512), 30: ("conv_x6b_kernel", 128, 128, 512),
     31: ("conv_x6b_kernel", 64, 128, 512), 32: ("conv_x6b_kernel", 64, 128, 512),
+    38: ("conv_x6b_kernel", 128, 64, 512), 39: ("conv_x6b_kernel", 128, 256, 512),
 }
 
 
@@ -672,10 +680,14 @@ def main():
     dist, rank, world = dist_setup(args.gpus)
     from edgeml_amd import models, synthetic
     from edgeml_amd import plan as plan_mod
-    stream = torch.cuda.Stream()
     out = {}
     if args.model in ("ssd", "both", "all"):
         B = args.ssd_batch
+        # fresh streams per model, created together with the other instances' (inflight_instances):
+        # consecutive streams land on distinct hardware queues; instances of a model placed on streams
+        # that share a queue are serialised against each other (an FRCNN run after the SSD one had two
+        # of its three instances on one queue: profiles/r4d_trace_both.jsonl)
+        stream = torch.cuda.Stream()
         m = models.ssdlite320_mobilenet_v3_large().to("cuda")
         plan = m.plan(B, 640, 640, u8)
         fill_input(plan, B, 100 * rank)
@@ -710,6 +722,11 @@ def main():
             m._slots.clear()
     if args.model in ("retinanet", "all"):
         B = args.retina_batch
+        # fresh streams per model, created together with the other instances' (inflight_instances):
+        # consecutive streams land on distinct hardware queues; instances of a model placed on streams
+        # that share a queue are serialised against each other (an FRCNN run after the SSD one had two
+        # of its three instances on one queue: profiles/r4d_trace_both.jsonl)
+        stream = torch.cuda.Stream()
         m = models.retinanet_resnet50_fpn_v2().to("cuda")
         plan = m.plan(B, 640, 640, u8)
         fill_input(plan, B, 100 * rank + 70)
@@ -725,6 +742,11 @@ def main():
         del plan
     if args.model in ("frcnn", "both", "all"):
         B = args.frcnn_batch
+        # fresh streams per model, created together with the other instances' (inflight_instances):
+        # consecutive streams land on distinct hardware queues; instances of a model placed on streams
+        # that share a queue are serialised against each other (an FRCNN run after the SSD one had two
+        # of its three instances on one queue: profiles/r4d_trace_both.jsonl)
+        stream = torch.cuda.Stream()
         m = models.fasterrcnn_resnet50_fpn_v2().to("cuda")
         plan = m.plan(B, 640, 640, u8)
         fill_input(plan, B, 100 * rank + 50)

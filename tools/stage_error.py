@@ -73,8 +73,9 @@ def main():
             row[f"rpn_obj{lvl}"] = (rel(heads_e[lvl][0], t["obj"][lvl]), rel(f["obj"][lvl], t["obj"][lvl]))
             row[f"rpn_del{lvl}"] = (rel(heads_e[lvl][1], t["del"][lvl]), rel(f["del"][lvl], t["del"][lvl]))
         row["box_scores"] = (float(np.abs(bsc_e - t["scores"]).max()), float(np.abs(f["scores"] - t["scores"]).max()))
-        for k, (e, r) in row.items():
+        for k, v in row.items():
             if k != "image":
+                e, r = v
                 print(f"image {i} {k:10s} engine {e:.3e}  f32 oracle {r:.3e}  ratio {e / max(r, 1e-30):7.2f}", flush=True)
         report.append(row)
     if a.o:
