@@ -261,11 +261,12 @@ __global__ void __launch_bounds__(256) dwconv_rb_group_kernel(DwGroup g) {
     dwconv_rb_body<K, S, PW>(g.p[k], g.nq[k], g.nwg[k], (int64_t)(bx - g.start[k]) * blockDim.x + threadIdx.x);
 }
 
-template <int K, int S, int PW>
+template <int K, int S, int PW, int QL = 16>
 __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, int nwg) {
-    __shared__ f32x4 red[16][16];
-    const int ql = threadIdx.x & 15, gl = threadIdx.x >> 4;
-    const int q = blockIdx.x * 16 + ql;
+    constexpr int GL = 256 / QL;  // group lanes per channel quad
+    __shared__ f32x4 red[GL][QL];
+    const int ql = threadIdx.x % QL, gl = threadIdx.x / QL;
+    const int q = blockIdx.x * QL + ql;
     const int c = q * 4;
     const int sidx = blockIdx.y, b = blockIdx.z;
     const int G = p.Ho * nwg;
@@ -275,7 +276,7 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
         const float* xb = p.x + (int64_t)b * p.H * p.W * p.C + c;
         const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + c);
         const int act = p.act;
-        for (int g = g0 + gl; g < g1; g += 16) {
+        for (int g = g0 + gl; g < g1; g += GL) {
             const int oh = g / nwg, ow0 = (g - oh * nwg) * PW;
             f32x4 acc[PW];
             dw_group<K, S, PW>(p, xb, oh, ow0, c, acc);
@@ -298,9 +299,26 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
     __syncthreads();
     if (gl == 0 && q < nq) {
         f32x4 t = red[0][ql];
-        for (int k = 1; k < 16; ++k) t += red[k][ql];
+        for (int k = 1; k < GL; ++k) t += red[k][ql];
         *reinterpret_cast<f32x4*>(p.part + ((int64_t)b * p.parts + sidx) * p.C + c) = t;
     }
+}
+
+// temporary A/B (round 4): EDGEDET_DW_SE = 0 (16 quads x 16 group lanes, 4 outputs per thread),
+// 1 (8 quads x 32 group lanes), 2 (16 x 16, 2 outputs per thread), 3 (8 x 32, 2 outputs)
+static int dw_se_variant() {
+    static const int v = [] {
+        const char* e = std::getenv("EDGEDET_DW_SE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int K, int S, int PW, int QL>
+static void dw_se_launch(const DwParams& p, hipStream_t s) {
+    const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
+    hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW, QL>), dim3((unsigned)cdiv(nq, QL), p.parts, p.B), dim3(256), 0, s,
+                       p, nq, nwg);
 }
 
 template <int K, int S>
@@ -308,8 +326,12 @@ static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
     constexpr int PW = 4;
     const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
     if (p.part) {
-        hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW>), dim3((unsigned)cdiv(nq, 16), p.parts, p.B), dim3(256), 0,
-                           s, p, nq, nwg);
+        switch (dw_se_variant()) {
+            case 1: dw_se_launch<K, S, 4, 8>(p, s); break;
+            case 2: dw_se_launch<K, S, 2, 16>(p, s); break;
+            case 3: dw_se_launch<K, S, 2, 8>(p, s); break;
+            default: dw_se_launch<K, S, 4, 16>(p, s); break;
+        }
     } else {
         const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
         hipLaunchKernelGGL((dwconv_rb_kernel<K, S, PW>), dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, nq,

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-4 session h: SE depthwise kernel variants (EDGEDET_DW_SE 0-3): the kernel tests per variant,
+# then alternated SSD runs with per-op times.
+cd "$GRAFT_REPO_ROOT" || exit 9
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
+: > gpurun_out/steps.log
+step() {  # step <name> <timeout> <cmd...>: stop on anything but success / test failure, and on faults
+    local name=$1 t=$2; shift 2
+    local t0=$SECONDS
+    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "[$name] rc=$rc $((SECONDS - t0)) s" >> gpurun_out/steps.log
+    if grep -q "illegal memory access\|Memory access fault\|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
+        echo "fault in $name: stopping" >> gpurun_out/steps.log; exit 7; fi
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
+    return 0
+}
+for v in 0 1 2 3; do
+  EDGEDET_DW_SE=$v step pytest_dwse$v 300 python -u -m pytest tests/test_gpu_kernels.py -q -x -k "dwconv" --timeout 120 --timeout-method thread
+  grep -q "failed" gpurun_out/pytest_dwse$v.log && { echo "variant $v fails its tests: stopping" >> gpurun_out/steps.log; exit 0; }
+done
+SSD_AB="bench.py --model ssd --steps 750 --warmup 20 --no-cpu --no-e2e --no-alt"
+for r in 1 2; do
+  o="0 1 2 3"; [ $r = 2 ] && o="3 2 1 0"
+  for v in $o; do EDGEDET_DW_SE=$v step ab_dwse${v}_r$r 300 python -u $SSD_AB --dump-ops gpurun_out/ops_dwse${v}_r$r.json; done
+done
+exit 0
