@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(256) dwconv_rb_group_kernel(DwGroup g) {
 
 template <int K, int S, int PW, int QL = 16>
 __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, int nwg) {
-    constexpr int GL = 256 / QL;  // group lanes per channel quad
+    constexpr int GL = 256 / QL;  // group lanes per channel quad (QL quads per workgroup)
     __shared__ f32x4 red[GL][QL];
     const int ql = threadIdx.x % QL, gl = threadIdx.x / QL;
     const int q = blockIdx.x * QL + ql;
@@ -304,34 +304,16 @@ __global__ void __launch_bounds__(256) dwconv_rb_se_kernel(DwParams p, int nq, i
     }
 }
 
-// temporary A/B (round 4): EDGEDET_DW_SE = 0 (16 quads x 16 group lanes, 4 outputs per thread),
-// 1 (8 quads x 32 group lanes), 2 (16 x 16, 2 outputs per thread), 3 (8 x 32, 2 outputs)
-static int dw_se_variant() {
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_DW_SE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
-template <int K, int S, int PW, int QL>
-static void dw_se_launch(const DwParams& p, hipStream_t s) {
-    const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
-    hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW, QL>), dim3((unsigned)cdiv(nq, QL), p.parts, p.B), dim3(256), 0, s,
-                       p, nq, nwg);
-}
-
 template <int K, int S>
 static int dwconv_rb_launch(const DwParams& p, hipStream_t s) {
     constexpr int PW = 4;
     const int nq = p.C / 4, nwg = cdiv(p.Wo, PW);
     if (p.part) {
-        switch (dw_se_variant()) {
-            case 1: dw_se_launch<K, S, 4, 8>(p, s); break;
-            case 2: dw_se_launch<K, S, 2, 16>(p, s); break;
-            case 3: dw_se_launch<K, S, 2, 8>(p, s); break;
-            default: dw_se_launch<K, S, 4, 16>(p, s); break;
-        }
+        // 16 channel quads x 16 group lanes per workgroup, 4 outputs per thread: against 8 x 32 and
+        // 2 outputs per thread, alternated SSD runs 31.59k / 31.48k vs 31.34k / 31.29k (8 x 32),
+        // 30.98k / 31.00k and 30.90k / 30.99k (2 outputs) (profiles/r4h_ab_dwse.txt)
+        hipLaunchKernelGGL((dwconv_rb_se_kernel<K, S, PW>), dim3((unsigned)cdiv(nq, 16), p.parts, p.B), dim3(256), 0,
+                           s, p, nq, nwg);
     } else {
         const int64_t total = (int64_t)p.B * p.Ho * nwg * nq;
         hipLaunchKernelGGL((dwconv_rb_kernel<K, S, PW>), dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, nq,
