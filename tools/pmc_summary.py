@@ -3,6 +3,9 @@
     python tools/pmc_summary.py --bench-log gpurun_out/bench_fetch_ssd.log --model ssd \
         --fetch gpurun_out/prof_fetch_ssd --write gpurun_out/prof_write_ssd -o profiles/pmc_ssd.json
 
+    (--kernel / --grid-wg / --algo-bytes / --launch: the same reduction for another launch, e.g. the
+    FRCNN box-head 3x3 convs: conv_x6b_kernel<false, true, false, 128, 1, false, 256>, 3,063 workgroups)
+
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one pass of TCC
 counters).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE on gfx950 reports exactly half of the bytes of
 a wide coalesced read, so it is doubled; WRITE_SIZE is taken as is; both are KiB.  The dispatches
@@ -53,11 +56,20 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("-o", required=True)
+    ap.add_argument("--kernel", default="", help="another launch than the roofline one: kernel name substring")
+    ap.add_argument("--grid-wg", type=int, default=0, help="... its grid in workgroups")
+    ap.add_argument("--wg-threads", type=int, default=512)
+    ap.add_argument("--algo-bytes", type=float, default=0.0, help="... its algorithmic bytes")
+    ap.add_argument("--launch", default="", help="... its name (for the record)")
     a = ap.parse_args()
-    line = bench_line(a.bench_log)
-    roof = line["roofline"] if a.model == "ssd" else line.get("frcnn", {}).get("roofline")
-    if roof is None and a.model == "frcnn":
-        roof = line["roofline"]
+    if a.kernel:
+        roof = {"kernel": a.kernel, "grid_wg": a.grid_wg, "wg_threads": a.wg_threads,
+                "algorithmic_bytes": a.algo_bytes, "launch": a.launch or a.kernel}
+    else:
+        line = bench_line(a.bench_log)
+        roof = line["roofline"] if a.model == "ssd" else line.get("frcnn", {}).get("roofline")
+        if roof is None and a.model == "frcnn":
+            roof = line["roofline"]
     kernel = roof["kernel"]
     grid = roof.get("grid_wg")
     items = grid * roof["wg_threads"] if grid else None
