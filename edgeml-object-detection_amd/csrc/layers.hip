@@ -1086,100 +1086,6 @@ __global__ void __launch_bounds__(512) se_fused_kernel(const float* __restrict__
     }
 }
 
-// Both excitation GEMMs of a wide SqueezeExcitation (C * S > 8192: SSDLite 480 / 672 channels) in
-// one launch on the fp32 matrix cores (v_mfma_f32_16x16x4_f32, exact fp32 products): workgroup =
-// (64 output channels, 16 images); the 16 images are the MFMA row dimension.
-//   squeeze  mean[16][C] (the partial sums in part order, / HW) into LDS;
-//   fc1      hidden[16][S] = relu(b1 + mean . w1^T): 16-wide S tiles over the 8 waves, K = C in
-//            4-deep steps (every workgroup computes all of it: 16 x S x C MACs, cheap next to the
-//            launch it saves);
-//   fc2      scale[16][64] = hardsigmoid(b2 + hidden . w2t[:, slice]): 4 channel tiles x 2 K halves
-//            over the 8 waves, the halves added in order.
-constexpr int SEW_IMG = 16, SEW_CH = 64, SEW_NT = 512;
-__global__ void __launch_bounds__(SEW_NT) se_wide_kernel(const float* __restrict__ part, const float* __restrict__ w1,
-                                                         const float* __restrict__ b1, const float* __restrict__ w2t,
-                                                         const float* __restrict__ b2, float* __restrict__ hidden,
-                                                         float* __restrict__ scale, int B, int C, int S, int HW,
-                                                         int parts) {
-    extern __shared__ __attribute__((aligned(16))) float sew_smem[];
-    const int CP = C + 1, SP = (S + 3) / 4 * 4 + 1;  // odd pitches
-    float* ms = sew_smem;                // [16][CP] squeeze means
-    float* hs = ms + SEW_IMG * CP;       // [16][SP] hidden (zero past S)
-    float* ps = hs + SEW_IMG * SP;       // [4][16][16] fc2 second-half partials
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15, q = lane >> 4;
-    const int b0 = blockIdx.y * SEW_IMG, nb = min(SEW_IMG, B - b0), c0 = blockIdx.x * SEW_CH;
-    const float inv = 1.f / (float)HW;
-    for (int t = tid; t < SEW_IMG * C; t += SEW_NT) {
-        const int bl = t / C, c = t - bl * C;
-        float acc = 0.f;
-        if (bl < nb) {
-            const float* pp = part + ((int64_t)(b0 + bl) * parts) * C + c;
-            for (int k = 0; k < parts; ++k) acc += pp[(int64_t)k * C];
-        }
-        ms[bl * CP + c] = acc * inv;
-    }
-    for (int t = tid; t < SEW_IMG * SP; t += SEW_NT) hs[t] = 0.f;
-    __syncthreads();
-    // fc1: tile n0 = 16 * tn over S, one wave per tile
-    const int ks1 = (C + 3) / 4;
-    for (int tn = wid; tn * 16 < S; tn += SEW_NT / 64) {
-        const int s_ = tn * 16 + l16;
-        const bool sv = s_ < S;
-        const float* wr = w1 + (int64_t)(sv ? s_ : 0) * C;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-        for (int k = 0; k < ks1; ++k) {
-            const int c = 4 * k + q;
-            const float a = c < C ? ms[l16 * CP + c] : 0.f;
-            const float w = sv && c < C ? wr[c] : 0.f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
-        }
-        if (sv) {
-            const float bv = b1[s_];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float t = acc[i] + bv;
-                hs[(4 * q + i) * SP + s_] = t > 0.f ? t : 0.f;  // row 4q + i = image, column = s
-            }
-        }
-    }
-    __syncthreads();
-    if (blockIdx.x == 0)
-        for (int t = tid; t < nb * S; t += SEW_NT) hidden[(int64_t)b0 * S + t] = hs[(t / S) * SP + t % S];
-    // fc2: channel tile tc (16 channels) x K half kh over S
-    const int tc = wid & 3, kh = wid >> 2, ks2 = (S + 3) / 4, kmid = (ks2 + 1) / 2;
-    const int c = c0 + 16 * tc + l16;
-    const bool cv = c < C;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = kh ? kmid : 0; k < (kh ? ks2 : kmid); ++k) {
-        const int j = 4 * k + q;
-        const float a = hs[l16 * SP + j];  // zero past S
-        const float w = cv && j < S ? w2t[(int64_t)j * C + c] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
-    }
-    if (kh) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ps[(tc * 16 + 4 * q + i) * 16 + l16] = acc[i];
-    }
-    __syncthreads();
-    if (!kh && cv) {
-        const float bv = b2[c];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 4 * q + i;
-            if (r < nb) scale[(int64_t)(b0 + r) * C + c] = apply_act((acc[i] + ps[(tc * 16 + r) * 16 + l16]) + bv, ACT_HSIGMOID);
-        }
-    }
-}
-
-static int se_wide_mode() {  // temporary A/B switch (round 4): EDGEDET_SE_WIDE=0 keeps the fc1 + fc2 pair
-    static const int v = [] {
-        const char* e = std::getenv("EDGEDET_SE_WIDE");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
-
 int se_fc_launch(const float* part, const float* w1, const float* b1, const float* w2t, const float* b2,
                  float* hidden, float* scale, int B, int C, int S, int HW, int parts, hipStream_t s) {
     if ((int64_t)C * S <= 8192 && parts >= 1 && parts <= SE_PARTS && S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX) {
@@ -1192,14 +1098,6 @@ int se_fc_launch(const float* part, const float* w1, const float* b1, const floa
     EDGEDET_REQUIRE(parts >= 1 && parts <= SE_PARTS, "se_fc: 1..16 squeeze partial sums");
     EDGEDET_REQUIRE(part && w1 && b1 && w2t && b2 && hidden && scale, "se_fc: null pointer");
     EDGEDET_REQUIRE(S >= 1 && S <= SE_SMAX && C >= 1 && C <= SE_CMAX && HW >= 1, "se_fc: C <= 1024, S <= 512");
-    if (se_wide_mode() == 1) {
-        const size_t lds = 4 * ((size_t)SEW_IMG * (C + 1) + (size_t)SEW_IMG * ((S + 3) / 4 * 4 + 1) + 4 * 16 * 16);
-        if (int rc = mbw_set_lds(se_wide_kernel, lds)) return rc;
-        hipLaunchKernelGGL(se_wide_kernel, dim3((unsigned)cdiv(C, SEW_CH), (unsigned)cdiv(B, SEW_IMG)), dim3(SEW_NT), lds,
-                           s, part, w1, b1, w2t, b2, hidden, scale, B, C, S, HW, parts);
-        EDGEDET_LAUNCH_CHECK();
-        return 0;
-    }
     EDGEDET_REQUIRE(C % 4 == 0 && S % 4 == 0 && ((uintptr_t)part & 15) == 0 && ((uintptr_t)w1 & 15) == 0 &&
                         ((uintptr_t)w2t & 15) == 0 && ((uintptr_t)hidden & 15) == 0,
                     "se_fc: C % 4, S % 4 and 16-byte aligned partial sums / weights / hidden (16-byte staging)");

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-4 session e: the bench timing check (per-pass completion traces), the bench as the driver
-# runs it and a long run, the FRCNN stage-error table, then the kernel trace, the PMC traffic passes
-# of the roofline launches and the MFMA utilisation passes.
+# One GPU session of record: parity tests + smoke, the bench as the driver runs it and a long run
+# (per-op times), the FRCNN stage-error table, the kernel trace, the PMC traffic passes of the
+# roofline launches (and the FRCNN box head) and the MFMA utilisation passes.  Steps stop the script
+# on a fault, a crash or a time limit.  Switches: TESTS BENCH STAGE PROF (1 = run, default all 1).
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
@@ -17,14 +18,9 @@ step() {  # step <name> <timeout> <cmd...>: stop on anything but success / test 
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc" >> gpurun_out/steps.log; exit $rc; fi
     return 0
 }
-if [ "${TESTS:-0}" = "1" ]; then
+if [ "${TESTS:-1}" = "1" ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
   step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
-fi
-rm -f gpurun_out/trace_*.jsonl
-if [ "${TRACE:-1}" = "1" ]; then
-  EDGEDET_BENCH_TRACE=gpurun_out/trace_frcnn.jsonl step tr_frcnn 300 python -u bench.py --model frcnn --steps 200 --warmup 10 --no-cpu --no-e2e --no-roofline --no-alt
-  EDGEDET_BENCH_TRACE=gpurun_out/trace_both.jsonl step tr_both 300 python -u bench.py --model both --steps 200 --warmup 10 --no-cpu --no-e2e --no-roofline --no-alt
 fi
 if [ "${BENCH:-1}" = "1" ]; then
   step bench_driver 900 python -u bench.py --gpus 1 --steps 20 --warmup 5
@@ -40,6 +36,7 @@ if [ "${PROF:-1}" = "1" ]; then
     step bench_write_$m 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$m -o write -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu --no-e2e
     python3 tools/pmc_summary.py --bench-log gpurun_out/bench_fetch_$m.log --model $m --fetch gpurun_out/prof_fetch_$m --write gpurun_out/prof_write_$m -o gpurun_out/pmc_$m.json >> gpurun_out/steps.log 2>&1
   done
+  python3 tools/pmc_summary.py --bench-log x --model frcnn --fetch gpurun_out/prof_fetch_frcnn --write gpurun_out/prof_write_frcnn -o gpurun_out/pmc_frcnn_boxhead.json --kernel "conv_x6b_kernel<false, true, false, 128, 1, false, 256>" --grid-wg 3063 --algo-bytes 805000000 --launch "roi_heads.box_head.{0..3}.0 (3x3, tile 39)" >> gpurun_out/steps.log 2>&1
   step mfma 600 bash tools/gpu_mfma.sh
 fi
 exit 0
