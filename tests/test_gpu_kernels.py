@@ -209,6 +209,45 @@ def test_ssd_stem_folded_transform_bit_identical(H0, W0, u8):
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+    if u8:  # the uint8 source (its 3 x 256 table) equals the host's float image / 255 as the source
+        srcf = (img8.float() / 255).to(DEV)
+        outf = torch.full_like(outs[1], float("nan"))
+        rf = rec[2:3].copy()
+        rf[0]["p"][9] = 0
+        rf[0]["p"][8] = srcf.data_ptr()
+        rf[0]["p"][7] = outf.data_ptr()
+        ops.check(ops.lib().edgedet_plan_run(rf.ctypes.data_as(ctypes.c_void_p), 1, ops.stream_handle()))
+        torch.cuda.synchronize()
+        assert torch.equal(outf, outs[1])
+
+
+@pytest.mark.parametrize("H0,W0", [(640, 640), (480, 640), (375, 500), (427, 640), (800, 1202)])
+def test_transform_u8_equals_float_image(H0, W0):
+    """The transform record on the decoded uint8 image (its 3 x 256 table of normalised values) equals
+    the transform of the host's float image / 255 (detect.py:58) bit for bit, with the FRCNN / RetinaNet
+    ImageNet normalisation (divisions that are not exact) and the SSD one."""
+    import ctypes
+    from edgeml_amd import ops
+    B = 2
+    g = torch.Generator().manual_seed(H0 * 7 + W0)
+    img8 = torch.randint(0, 256, (B, 3, H0, W0), generator=g, dtype=torch.uint8)
+    Ho, Wo = (H0 * 2 // 3, W0 * 2 // 3) if H0 > 700 else (H0 + 37, W0 + 41)
+    for norm in ([0.485, 0.456, 0.406, 0.229, 0.224, 0.225], [0.5] * 6):
+        outs = []
+        for u8 in (True, False):
+            src = (img8 if u8 else img8.float() / 255).to(DEV)
+            x4 = torch.full((B, Ho, Wo, 4), float("nan"), device=DEV)
+            rec = np.zeros(1, dtype=ops.OP_DTYPE)
+            rec[0]["kind"] = ops.PREPROCESS
+            rec[0]["i"][:7] = [B, H0, W0, Ho, Wo, Ho, Wo]
+            rec[0]["p"][2 if u8 else 0] = src.data_ptr()
+            rec[0]["p"][1] = x4.data_ptr()
+            rec[0]["f"][:6] = norm
+            ops.check(ops.lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), 1, ops.stream_handle()))
+            torch.cuda.synchronize()
+            outs.append(x4.cpu())
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1]), (norm, int((outs[0] != outs[1]).sum()))
 
 
 @pytest.mark.parametrize("B,C,S,parts", [(1, 72, 24, 16), (32, 960, 240, 1), (7, 120, 32, 5), (64, 672, 168, 2),
@@ -449,3 +488,23 @@ def test_mbconv_block_matches_torch(B, H, W, Cin, E, Cout, k, s, act):
     got = yd.cpu()
     err = (got - ref).abs().max().item()
     assert torch.isfinite(got).all() and err <= 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("n,so,do", [(1, 0, 0), (15, 0, 0), (16, 0, 0), (4099, 0, 0), (3 * 2 ** 20 + 5, 0, 0),
+                                     (4099, 3, 3), (70001, 5, 9), (0, 0, 0)])
+def test_upload_kernel_copies_exactly(n, so, do):
+    """ops.upload (edgedet_upload: the batch input upload as a kernel on the consuming stream) copies a
+    pinned host buffer, or a device buffer, byte for byte, at any length and alignment offsets."""
+    from edgeml_amd import ops
+    g = torch.Generator().manual_seed(n + so)
+    host = torch.randint(0, 256, (n + so,), generator=g, dtype=torch.uint8).pin_memory()
+    dst = torch.zeros(n + do + 7, dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream()
+    ops.upload([(dst[do:do + n], host[so:so + n])], s)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[do:do + n].cpu(), host[so:so + n])
+    assert int(dst[:do].sum()) == 0 and int(dst[do + n:].sum()) == 0
+    dev2 = torch.zeros_like(dst)
+    ops.upload([(dev2[do:do + n], dst[do:do + n])], s)
+    torch.cuda.synchronize()
+    assert torch.equal(dev2, dst)
