@@ -87,12 +87,7 @@ __device__ __forceinline__ f32x4 pre_pixel_lut(const uint8_t* __restrict__ xb, i
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) preprocess_kernel(PreParams p, const T* __restrict__ x) {
-    __shared__ float lut[sizeof(T) == 1 ? 3 * 256 : 1];  // uint8 source: pre_pixel_lut's table
-    if constexpr (sizeof(T) == 1) {
-        for (int e = threadIdx.x; e < 3 * 256; e += 256) lut[e] = ((float)(e & 255) / 255.f - p.mean[e >> 8]) / p.stdv[e >> 8];
-        __syncthreads();
-    }
+__global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
     if (idx >= total) return;
@@ -100,12 +95,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreParams p, const T* _
     const int oy = (int)((idx / p.Wp) % p.Hp);
     const int b = (int)(idx / ((int64_t)p.Wp * p.Hp));
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
-    if (oy < p.Ho && ox < p.Wo) {
-        if constexpr (sizeof(T) == 1)
-            out = pre_pixel_lut(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, lut, oy, ox);
-        else
-            out = pre_pixel(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, p.mean, p.stdv, oy, ox);
-    }
+    if (oy < p.Ho && ox < p.Wo) out = pre_pixel(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, p.mean, p.stdv, oy, ox);
     *reinterpret_cast<f32x4*>(p.y + idx * 4) = out;
 }
 
