@@ -58,34 +58,6 @@ __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int 
     return f32x4{v[0], v[1], v[2], 0.f};
 }
 
-// The same pixel from a uint8 image through a table of the 3 x 256 normalised values,
-// lut[c][v] = ((float)v / 255 - mean[c]) / stdv[c], each computed with pre_pixel's own operations:
-// the same bits without the 24 IEEE divisions per pixel.
-__device__ __forceinline__ f32x4 pre_pixel_lut(const uint8_t* __restrict__ xb, int H, int W, float sh, float sw,
-                                               const float* lut, int oy, int ox) {
-    float ry = sh * ((float)oy + 0.5f) - 0.5f;
-    float rx = sw * ((float)ox + 0.5f) - 0.5f;
-    ry = ry < 0.f ? 0.f : ry;
-    rx = rx < 0.f ? 0.f : rx;
-    const int y0 = (int)ry, x0 = (int)rx;
-    const int y1 = y0 + ((y0 < H - 1) ? 1 : 0);
-    const int x1 = x0 + ((x0 < W - 1) ? 1 : 0);
-    const float ly = ry - (float)y0, lx = rx - (float)x0;
-    const float hy = 1.f - ly, hx = 1.f - lx;
-    float v[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const uint8_t* src = xb + (int64_t)c * H * W;
-        const float* t = lut + 256 * c;
-        const float a00 = t[src[(int64_t)y0 * W + x0]];
-        const float a01 = t[src[(int64_t)y0 * W + x1]];
-        const float a10 = t[src[(int64_t)y1 * W + x0]];
-        const float a11 = t[src[(int64_t)y1 * W + x1]];
-        v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
-    }
-    return f32x4{v[0], v[1], v[2], 0.f};
-}
-
 template <typename T>
 __global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -372,17 +344,12 @@ constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 
 // T = float: the transform's NHWC4 output (p.x); T = float / uint8_t with FUSED: the source image
 // (p.src / p.src8, [B][3][H0][W0]) and the transform computed per input pixel of the tile (pre_pixel,
 // the same bits as the transform kernel): no transform launch and no NHWC4 round trip through HBM.
-template <typename T, bool FUSED, bool LUT = true>
+template <typename T, bool FUSED>
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
     __shared__ __attribute__((aligned(16))) float ws[STEM_NW];
-    __shared__ float lut[sizeof(T) == 1 && FUSED && LUT ? 3 * 256 : 1];  // uint8 source: pre_pixel_lut's table
     const int tid = threadIdx.x, b = blockIdx.y;
-    if constexpr (sizeof(T) == 1 && FUSED && LUT) {
-        for (int e = tid; e < 3 * 256; e += 256) lut[e] = ((float)(e & 255) / 255.f - p.mean[e >> 8]) / p.stdv[e >> 8];
-        __syncthreads();
-    }
     const int oh0 = (blockIdx.x / tiles_w) * STEM_T, ow0 = (blockIdx.x % tiles_w) * STEM_T;
     const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
     const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
@@ -410,11 +377,7 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             if constexpr (FUSED) {
                 const T* img = (const T*)(sizeof(T) == 1 ? (const void*)p.src8 : (const void*)p.src) +
                                (int64_t)b * 3 * p.H0 * p.W0;
-                if constexpr (sizeof(T) == 1 && LUT)
-                    xv[r] = in ? pre_pixel_lut(p.src8 + (int64_t)b * 3 * p.H0 * p.W0, p.H0, p.W0, p.sh, p.sw, lut, ih, iw)
-                               : f32x4{0.f, 0.f, 0.f, 0.f};
-                else
-                    xv[r] = in ? pre_pixel(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, ih, iw) : f32x4{0.f, 0.f, 0.f, 0.f};
+                xv[r] = in ? pre_pixel(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, ih, iw) : f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
                 const float* src = xb + (in ? ((int64_t)ih * p.W + iw) * 4 : 0);  // clamped: loads stay unconditional
                 xv[r] = *reinterpret_cast<const f32x4*>(src);
@@ -518,11 +481,7 @@ int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
     EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
     const int tiles_w = cdiv(p.Wo, STEM_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B);
-    static const bool lut = [] {  // temporary A/B switch (round 4): EDGEDET_STEM_LUT=0 divides per tap
-        const char* e = std::getenv("EDGEDET_STEM_LUT");
-        return !(e && e[0] == '0');
-    }();
-    void (*k)(StemParams, int) = p.src8 ? (lut ? ssd_stem_kernel<uint8_t, true> : ssd_stem_kernel<uint8_t, true, false>)
+    void (*k)(StemParams, int) = p.src8 ? ssd_stem_kernel<uint8_t, true>
                                  : p.src ? ssd_stem_kernel<float, true> : ssd_stem_kernel<float, false>;
     hipLaunchKernelGGL(k, grid, dim3(256), 0, s, p, tiles_w);
     EDGEDET_LAUNCH_CHECK();
