@@ -66,11 +66,10 @@ def d2h_buffers(plan):
 
 
 def step(plan, stream, d2h):
-    """One pass: the plan's graph, then its detections to the pinned host buffers (ops.download, the
-    product path's results copy)."""
-    from edgeml_amd import ops
     plan.replay(stream)
-    ops.download([(host, dev) for dev, host in d2h], stream)
+    with torch.cuda.stream(stream):
+        for dev, host in d2h:
+            host.copy_(dev, non_blocking=True)
 
 
 TIMING = {}  # how the last timed_steps call measured (reported on the JSON line)

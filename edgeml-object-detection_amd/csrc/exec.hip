@@ -53,7 +53,6 @@
 //                  i0..4 B,L,kin,K,kmax; d0 iou
 //   FORK / JOIN    i0 number of side lanes; i47 of every other record = its lane (0 = caller's stream)
 //   WAIT           lane i0 waits for everything issued so far on lane i1 (both forked, or 0)
-#include <algorithm>
 #include <cstdlib>
 #include <memory>
 #include <mutex>
@@ -593,26 +592,9 @@ static int run_group(const edgedet_op* m, int n, hipStream_t s) {
     return 0;
 }
 
-// One empty workgroup on the caller's stream ahead of a plan that opens with a FORK: the side lanes'
-// first kernels then hang off a node that is ordered behind the stream's earlier work (the input's
-// host-to-device copy), instead of being roots of the captured graph.
-__global__ void lane_head_kernel() {}
-
-static int head_mode() {
-    static const int m = [] {
-        const char* e = std::getenv("EDGEDET_GRAPH_HEAD");
-        return e ? std::atoi(e) : 1;
-    }();
-    return m;
-}
-
 static int run_ops(const edgedet_op* ops, int64_t n, hipStream_t s) {
     const int64_t waits = check_topology(ops, n);
     if (waits < 0) return (int)waits;
-    if (n > 0 && (head_mode() >= 2 || (head_mode() == 1 && ops[0].kind == EDGEDET_OP_FORK))) {
-        hipLaunchKernelGGL(lane_head_kernel, dim3(1), dim3(64), 0, s);
-        EDGEDET_LAUNCH_CHECK();
-    }
     bool need_lanes = false;
     for (int64_t k = 0; k < n && !need_lanes; ++k)
         need_lanes = ops[k].kind == EDGEDET_OP_FORK || ops[k].i[EDGEDET_OP_LANE] != 0;
@@ -738,101 +720,6 @@ extern "C" int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stre
         g_graphs.insert(g);
     }
     *out = g;
-    return 0;
-}
-
-// Upload: a grid of 512 workgroups streaming 16-byte words (4 in flight per thread, enough to cover
-// the bus latency), bytes at the unaligned ends (or throughout, when source and destination are not
-// aligned alike: never for the engine's pinned batches and 256-byte aligned inputs).  The source is
-// read with system-scope loads, which always reach memory: pinned host buffers are rewritten by the
-// host between uploads (the detect CLI's recycled batch buffers, run_batches' per-slot staging), and a
-// plain load may hit a line the device cached from the buffer's previous contents.
-namespace edgedet {
-__device__ __forceinline__ unsigned long long load_sys8(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint8_t load_sys1(const uint8_t* p) {  // the aligned word holding the byte
-    const uintptr_t a = (uintptr_t)p;
-    const unsigned w = __hip_atomic_load(reinterpret_cast<const unsigned*>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
-    return (uint8_t)(w >> (8 * (a & 3)));
-}
-__device__ __forceinline__ uint4 load_sys16(const unsigned long long* p) {
-    const unsigned long long lo = load_sys8(p), hi = load_sys8(p + 1);
-    return uint4{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
-}
-__global__ void __launch_bounds__(256) upload_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                     int64_t head, int64_t n16, int64_t n) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, T = (int64_t)gridDim.x * 256;
-    if (t < head) dst[t] = load_sys1(src + t);
-    const unsigned long long* s8 = reinterpret_cast<const unsigned long long*>(src + head);
-    uint4* d4 = reinterpret_cast<uint4*>(dst + head);
-    int64_t i = t;
-    for (; i + 3 * T < n16; i += 4 * T) {
-        const uint4 a = load_sys16(s8 + 2 * i), b = load_sys16(s8 + 2 * (i + T)), c = load_sys16(s8 + 2 * (i + 2 * T)),
-                    d = load_sys16(s8 + 2 * (i + 3 * T));
-        d4[i] = a;
-        d4[i + T] = b;
-        d4[i + 2 * T] = c;
-        d4[i + 3 * T] = d;
-    }
-    for (; i < n16; i += T) d4[i] = load_sys16(s8 + 2 * i);
-    for (int64_t j = head + 16 * n16 + t; j < n; j += T) dst[j] = load_sys1(src + j);
-}
-// Download: device results into pinned host memory with system-scope stores (written through to
-// memory, so the host reads them once the stream's event has completed); 4-byte words.
-__global__ void __launch_bounds__(256) download_kernel(const unsigned* __restrict__ src, unsigned* __restrict__ dst,
-                                                       int64_t n4) {
-    const int64_t T = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += T)
-        __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-static int upload_grid() {
-    static const int g = [] {
-        const char* e = std::getenv("EDGEDET_UPLOAD_GRID");  // measurement knob (tools/upload_bw.py)
-        return e ? std::max(1, std::atoi(e)) : 512;
-    }();
-    return g;
-}
-}  // namespace edgedet
-
-extern "C" int edgedet_download(const void* src, void* dst, int64_t nbytes, void* stream) {
-    if (nbytes == 0) return 0;
-    EDGEDET_REQUIRE(src && dst && nbytes > 0 && nbytes % 4 == 0 && ((uintptr_t)src & 3) == 0 && ((uintptr_t)dst & 3) == 0,
-                    "download: null pointer, or a size / address that is not a multiple of 4 bytes");
-    void* ddst = nullptr;
-    if (hipHostGetDevicePointer(&ddst, dst, 0) != hipSuccess || !ddst) {
-        (void)hipGetLastError();
-        ddst = dst;
-    }
-    const int64_t n4 = nbytes / 4;
-    const unsigned grid = (unsigned)std::min<int64_t>(256, (n4 + 255) / 256);
-    hipLaunchKernelGGL(download_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       static_cast<const unsigned*>(src), static_cast<unsigned*>(ddst), n4);
-    EDGEDET_LAUNCH_CHECK();
-    return 0;
-}
-
-extern "C" int edgedet_upload(const void* src, void* dst, int64_t nbytes, void* stream) {
-    if (nbytes == 0) return 0;
-    EDGEDET_REQUIRE(src && dst && nbytes > 0, "upload: null pointer or negative size");
-    void* dsrc = nullptr;  // pinned host memory's device address (the same address under ROCm's UVA)
-    if (hipHostGetDevicePointer(&dsrc, const_cast<void*>(src), 0) != hipSuccess || !dsrc) {
-        (void)hipGetLastError();
-        dsrc = const_cast<void*>(src);
-    }
-    const uint8_t* s = static_cast<const uint8_t*>(dsrc);
-    uint8_t* d = static_cast<uint8_t*>(dst);
-    // 16-byte words where source and destination share their alignment; bytes otherwise
-    int64_t head = 0, n16 = 0;
-    if (((uintptr_t)s & 15) == ((uintptr_t)d & 15)) {
-        head = std::min<int64_t>(nbytes, (16 - ((uintptr_t)d & 15)) & 15);
-        n16 = (nbytes - head) / 16;
-    }
-    hipLaunchKernelGGL(upload_kernel, dim3((unsigned)upload_grid()), dim3(256), 0, (hipStream_t)stream, s, d, head, n16,
-                       nbytes);
-    EDGEDET_LAUNCH_CHECK();
     return 0;
 }
 

@@ -141,7 +141,6 @@ class BatchDecoder:
         self.dev = torch.empty(0, dtype=torch.uint8, device=self.device)
         self.planes = torch.empty(0, dtype=torch.uint8, device=self.device)
         self.done = None
-        self.hold = None  # the last call's host packets (the upload kernel reads them in place)
 
     def decode(self, packets, out, stream=None):
         if isinstance(packets, PackedBatch):
@@ -180,12 +179,11 @@ class BatchDecoder:
             for p, o, n in zip(packets, offs, sizes):
                 st[o:o + n] = p.numpy() if torch.is_tensor(p) else p
         s = stream or torch.cuda.current_stream(self.device)
-        pairs = [(self.dev[:staged], self.stage[:staged])]
-        if direct:  # the caching host allocator keeps each packet's block until its copy is done
-            pairs += [(self.dev[int(o):int(o) + n], p) for p, o, n in zip(packets, offs, sizes)]
-        ops.upload(pairs, s)  # read by a kernel: the packets are held until the next call's wait
-        self.hold = packets
         with torch.cuda.stream(s):
+            self.dev[:staged].copy_(self.stage[:staged], non_blocking=True)
+            if direct:  # the caching host allocator keeps each packet's block until its copy is done
+                for p, o, n in zip(packets, offs, sizes):
+                    self.dev[int(o):int(o) + n].copy_(p, non_blocking=True)
             base = self.dev.data_ptr()
             ops.check(ops.lib().edgedet_jpeg_decode_batch(ctypes.c_void_p(base), ctypes.c_void_p(base), B, H, W,
                                                            max(blocks), ctypes.c_void_p(self.planes.data_ptr()),
@@ -196,8 +194,8 @@ class BatchDecoder:
         return out
 
     def decode_packed(self, pb, out, stream=None):
-        """A PackedBatch: one upload of its span (ops.upload), then the device reconstruction into out.
-        pb is held until the next call, which first waits for this one's kernels."""
+        """A PackedBatch: one H2D copy of its span, then the device reconstruction into out.  The
+        caching host allocator keeps pb.buf's block until the copy has run."""
         B, C, H, W = out.shape
         if C != 3 or out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or len(pb) != B or \
                 pb.hw != (H, W):
@@ -207,17 +205,12 @@ class BatchDecoder:
         stride = (pb.plane_bytes + 255) // 256 * 256
         if self.planes.numel() < B * stride:
             self.planes = torch.empty(B * stride * 2, dtype=torch.uint8, device=self.device)
-        if self.done is not None:
-            self.done.synchronize()  # the previous batch's kernels are done with its buffers
         s = stream or torch.cuda.current_stream(self.device)
-        ops.upload([(self.dev[:pb.span], pb.buf[:pb.span])], s)  # read by a kernel: pb is held
-        self.hold = pb
         with torch.cuda.stream(s):
+            self.dev[:pb.span].copy_(pb.buf[:pb.span], non_blocking=True)
             base = self.dev.data_ptr()
             ops.check(ops.lib().edgedet_jpeg_decode_batch(ctypes.c_void_p(base), ctypes.c_void_p(base), B, H, W,
                                                            pb.plane_bytes // 64, ctypes.c_void_p(self.planes.data_ptr()),
                                                            stride, ctypes.c_void_p(out.data_ptr()),
                                                            ops.stream_handle(s)))
-            self.done = torch.cuda.Event()
-            self.done.record(s)
         return out

@@ -26,9 +26,6 @@ from . import native
 from . import ops
 from .plan import NativePlan
 
-import os as _os
-_DIAG = int(_os.environ.get("EDGEDET_RB_DIAG", "0"))  # temporary diagnostic switch
-
 
 def _check_keys(sd, table, what):
     missing = [k for k in table if k not in sd]
@@ -132,8 +129,6 @@ class _Detector:
                 for j, idx in enumerate(chunk):
                     inp[j].copy_(imgs[idx].to(self.device, torch.float32), non_blocking=True)
                 plan.run()
-                # the host waits for the plan (its side lanes included) before the results' copies
-                torch.cuda.current_stream(self.device).synchronize()
                 counts = plan.out_count.tensor().cpu().tolist()
                 boxes = plan.out_box.tensor()
                 scores = plan.out_score.tensor()
@@ -270,13 +265,7 @@ class _Detector:
             lap("issue")
             if plan.graph is None:
                 # one hipGraph per slot plan (captured on first use): a batch is then one launch
-                # instead of a host call per op, which kept the host, not the device, the bottleneck.
-                # The capture (its eager warm-up run and priming replays) runs on an idle device: with
-                # another slot's batch in flight during it, a later batch of the SSD two-chain plans
-                # measured differing results (tools/race_check.py, profiles/r4k_upload_race.txt)
-                while pending:
-                    yield from emit(pending.pop(0))
-                torch.cuda.synchronize(self.device)
+                # instead of a host call per op, which kept the host, not the device, the bottleneck
                 plan.capture(stream)
             lap("plans")
             with torch.cuda.stream(stream):
@@ -284,27 +273,13 @@ class _Detector:
                     if sl["jpeg"] is None:
                         sl["jpeg"] = BatchDecoder(self.device)
                     sl["jpeg"].decode(imgs, plan.input.tensor(), stream)
-                elif _DIAG & 8:
+                else:
                     plan.input.tensor().copy_(src, non_blocking=True)
-                else:
-                    ops.upload([(plan.input.tensor(), src)], stream)
-                if _DIAG & 1:
-                    stream.synchronize()
-                if _DIAG & 4:
-                    plan.run(stream)
-                else:
-                    plan.replay(stream)
-                if _DIAG & 2:
-                    stream.synchronize()
-                if _DIAG & 16:
-                    sl["count"].copy_(plan.out_count.tensor(), non_blocking=True)
-                    sl["box"].copy_(plan.out_box.tensor(), non_blocking=True)
-                    sl["score"].copy_(plan.out_score.tensor(), non_blocking=True)
-                    sl["label"].copy_(plan.out_label.tensor(), non_blocking=True)
-                else:
-                    ops.download([(sl["count"], plan.out_count.tensor()), (sl["box"], plan.out_box.tensor()),
-                                  (sl["score"], plan.out_score.tensor()), (sl["label"], plan.out_label.tensor())],
-                                 stream)
+                plan.replay(stream)
+                sl["count"].copy_(plan.out_count.tensor(), non_blocking=True)
+                sl["box"].copy_(plan.out_box.tensor(), non_blocking=True)
+                sl["score"].copy_(plan.out_score.tensor(), non_blocking=True)
+                sl["label"].copy_(plan.out_label.tensor(), non_blocking=True)
                 sl["done"].record(stream)
             pending.append((tag, sl, B))
             while len(pending) >= n:

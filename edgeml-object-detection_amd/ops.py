@@ -57,8 +57,7 @@ EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "
            "edgedet_frcnn_workspace_size", "edgedet_frcnn_forward", "edgedet_plan_check", "edgedet_release_lanes",
            "edgedet_lane_sets", "edgedet_nms_workspace_size", "edgedet_nms_ws", "edgedet_batched_nms_ws",
            "edgedet_topk_segments", "edgedet_box_decode", "edgedet_jpeg_packet", "edgedet_jpeg_batch_packets", "edgedet_jpeg_plane_bytes", "edgedet_image_dims",
-           "edgedet_jpeg_decode_batch", "edgedet_jpeg_reconstruct_host", "edgedet_model_buffers", "edgedet_model_op_names", "edgedet_model_release",
-           "edgedet_upload", "edgedet_download")
+           "edgedet_jpeg_decode_batch", "edgedet_jpeg_reconstruct_host", "edgedet_model_buffers", "edgedet_model_op_names", "edgedet_model_release")
 
 
 class EdgeDetUnavailable(RuntimeError):
@@ -93,8 +92,6 @@ def lib():
     L.edgedet_graph_create.argtypes = [_vp, _i64, _vp, ctypes.POINTER(_vp)]
     L.edgedet_graph_launch.argtypes = [_vp, _vp]
     L.edgedet_graph_destroy.argtypes = [_vp]
-    L.edgedet_upload.argtypes = [_vp, _vp, _i64, _vp]
-    L.edgedet_download.argtypes = [_vp, _vp, _i64, _vp]
     L.edgedet_nms.argtypes = [_vp, _vp, _i64, _dbl, _vp, _vp, _vp]
     L.edgedet_batched_nms.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp]
     L.edgedet_nms_workspace_size.argtypes = [_i64]
@@ -182,50 +179,6 @@ def check(rc):
 def stream_handle(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
-
-
-def upload(pairs, stream):
-    """dst.copy_(src) for each (dst, src) of pairs, ordered ahead of `stream`'s later kernels.
-
-    A pinned-host (or device) source is copied by the library's upload kernel on `stream`
-    (edgedet_upload: the compute units read the host memory over the bus), not by the system DMA
-    engines.  Measured on the MI355X box (tools/race_check.py, profiles/r4k_upload_race.txt): with
-    another batch's kernels running on a second stream, a non_blocking DMA copy on the consuming stream
-    (or on a stream of its own, waited for through an event) was at times still landing when the
-    kernels queued behind it read the input: 2-5% of the images of the second in-flight slot differed,
-    always the images the copy writes last.  With the DMA engines disabled (HSA_ENABLE_SDMA=0: copies
-    by kernels) or the host waiting for the copy, the same runs were exact.  A pageable host source
-    is copied synchronously by torch."""
-    L = lib()
-    for dst, src in pairs:
-        if not (dst.is_cuda and dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype
-                and dst.shape == src.shape):
-            raise ValueError("upload: dst must be a contiguous cuda tensor of src's dtype and shape")
-        if src.numel() == 0:
-            continue
-        if src.is_cuda or src.is_pinned():
-            check(L.edgedet_upload(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
-                                   src.numel() * src.element_size(), stream_handle(stream)))
-        else:
-            with torch.cuda.stream(stream):
-                dst.copy_(src)
-
-
-def download(pairs, stream):
-    """host.copy_(dev) for each (host, dev) of pairs after `stream`'s earlier kernels: the library's
-    download kernel (edgedet_download, system-scope stores into the pinned host buffers) instead of a
-    DMA copy, whose ordering behind another stream's kernels (the side lanes' JOIN) was not kept in the
-    measured runs (tools/race_check.py: SSD 16-image batches on two chains, two batches in flight, 1-6%
-    of images differing; exact with the host waiting for the stream before the copy).  The host reads
-    the buffers after an event recorded on `stream` behind this call."""
-    L = lib()
-    for host, dev in pairs:
-        if not (dev.is_cuda and host.is_pinned() and host.is_contiguous() and dev.is_contiguous()
-                and host.dtype == dev.dtype and host.shape == dev.shape):
-            raise ValueError("download: host must be a pinned contiguous tensor of the device tensor's dtype and shape")
-        if dev.numel():
-            check(L.edgedet_download(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(host.data_ptr()),
-                                     dev.numel() * dev.element_size(), stream_handle(stream)))
 
 
 def _ptr(t):

@@ -104,17 +104,6 @@ int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** 
 int edgedet_graph_launch(void* graph, void* stream);
 int edgedet_graph_destroy(void* graph);
 
-/* Copy nbytes from src (pinned host memory, hipHostMalloc'd or registered, or device memory) to the
- * device buffer dst with a kernel on `stream` (the compute units read the host memory over the bus).
- * A batch's input upload, ordered ahead of the stream's later kernels like any kernel: the
- * system-DMA form of the same copy (hipMemcpyAsync) was at times still landing when a kernel queued
- * behind it read the buffer, with another stream busy (profiles/r4k_upload_race.txt). */
-int edgedet_upload(const void* src, void* dst, int64_t nbytes, void* stream);
-/* The results' way back: nbytes (a multiple of 4, 4-byte aligned) from device memory src into pinned
- * host memory dst, by a kernel on `stream` with system-scope stores; the host reads dst after an event
- * recorded on `stream` behind it has completed. */
-int edgedet_download(const void* src, void* dst, int64_t nbytes, void* stream);
-
 /* ------------------------------------------------------------------------ model forward */
 /*
  * The detector call of torch_models/detect.py:78 (model(images) -> boxes / scores / labels for the

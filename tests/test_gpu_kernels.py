@@ -488,23 +488,3 @@ def test_mbconv_block_matches_torch(B, H, W, Cin, E, Cout, k, s, act):
     got = yd.cpu()
     err = (got - ref).abs().max().item()
     assert torch.isfinite(got).all() and err <= 1e-4 * max(1.0, ref.abs().max().item()), err
-
-
-@pytest.mark.parametrize("n,so,do", [(1, 0, 0), (15, 0, 0), (16, 0, 0), (4099, 0, 0), (3 * 2 ** 20 + 5, 0, 0),
-                                     (4099, 3, 3), (70001, 5, 9), (0, 0, 0)])
-def test_upload_kernel_copies_exactly(n, so, do):
-    """ops.upload (edgedet_upload: the batch input upload as a kernel on the consuming stream) copies a
-    pinned host buffer, or a device buffer, byte for byte, at any length and alignment offsets."""
-    from edgeml_amd import ops
-    g = torch.Generator().manual_seed(n + so)
-    host = torch.randint(0, 256, (n + so,), generator=g, dtype=torch.uint8).pin_memory()
-    dst = torch.zeros(n + do + 7, dtype=torch.uint8, device=DEV)
-    s = torch.cuda.current_stream()
-    ops.upload([(dst[do:do + n], host[so:so + n])], s)
-    torch.cuda.synchronize()
-    assert torch.equal(dst[do:do + n].cpu(), host[so:so + n])
-    assert int(dst[:do].sum()) == 0 and int(dst[do + n:].sum()) == 0
-    dev2 = torch.zeros_like(dst)
-    ops.upload([(dev2[do:do + n], dst[do:do + n])], s)
-    torch.cuda.synchronize()
-    assert torch.equal(dev2, dst)

@@ -52,7 +52,7 @@ def main():
                              if ref[t][j][0].shape == b.shape and np.array_equal(ref[t][j][0], b)]
                     top = float(np.abs(b[:1] - rb[:1]).max()) if len(b) and len(rb) else -1.0
                     bad.append((tag, j, "stale%s" % stale if stale else "top%.3g" % top))
-        print(f"rep {rep} path {a.path} B {a.B} head {os.environ.get('EDGEDET_GRAPH_HEAD', 'default')}: "
+        print(f"rep {rep} path {a.path} B {a.B}: "
               f"{len(bad)} differing images of {a.n * a.B}: {bad[:12]}", flush=True)
 
 
