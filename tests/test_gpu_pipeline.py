@@ -162,3 +162,29 @@ def test_run_batches_matches_call(kind):
             np.testing.assert_array_equal(su, s)
             np.testing.assert_array_equal(lu, l)
             assert len(s) > 0
+
+
+@pytest.mark.parametrize("kind,B,H,W,inflight,n", [("ssd", 32, 640, 640, 4, 8), ("ssd", 8, 480, 640, 2, 8),
+                                                   ("frcnn", 6, 427, 640, 3, 6)])
+def test_run_batches_in_flight_reproducible(kind, B, H, W, inflight, n):
+    """With the models' own in-flight counts (SSD: 32-image batches on two 16-image chains, four in
+    flight; FRCNN: three in flight) every image's detections equal the one-batch-at-a-time result.
+    Round 4's uint8 table kernels failed exactly this (profiles/r4k_lut_race.txt: whole batches or
+    single images differing under concurrency, while every single-kernel parity test passed)."""
+    from edgeml_amd import models, synthetic
+    if kind == "ssd":
+        model = models.SSDLite320(synthetic.synthetic_state_dict("ssd", 91, True, seed=0), 91, True).to("cuda:0")
+    else:
+        model = models.fasterrcnn_resnet50_fpn_v2().to("cuda:0")
+    u8s = [synthetic.make_batch_u8(B, H, W, seed=300 + i) for i in range(n)]
+    ref = [model(list(u.float() / 255)) for u in u8s]
+    for rep in range(2):
+        got = list(model.run_batches([(i, u.pin_memory() if rep else list(u)) for i, u in enumerate(u8s)],
+                                     inflight=inflight))
+        assert [t for t, _ in got] == list(range(n))
+        for (t, dets) in got:
+            for j, (b, s, l) in enumerate(dets):
+                r = ref[t][j]
+                np.testing.assert_array_equal(b, r["boxes"].cpu().numpy(), err_msg=f"rep {rep} batch {t} image {j}")
+                np.testing.assert_array_equal(s, r["scores"].cpu().numpy())
+                np.testing.assert_array_equal(l, r["labels"].cpu().numpy())
