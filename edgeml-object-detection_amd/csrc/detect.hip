@@ -1144,11 +1144,16 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 // ================================================================ RPN per-level selection
 
 // rpn_chunk_select_kernel: one workgroup per (chunk of P.chunk anchors, level, image) keeps the
-// chunk's top-k logits (ties in index order) unsorted, in index order, with their level indices.  Every
-// element of a level's top-k is in its chunk's top-k, so the union of the chunk lists, chunks in order,
-// holds the level's top-k with the index order preserved: the level kernel then selects from at most
-// nchunk x KC entries instead of streaming the whole level (120,000 logits per image at P2) through its
-// five radix passes.
+// chunk's top-k logits (ties at the cut in index order) unsorted, with their level indices.  compact()
+// writes the list in two classes -- the keys above the chunk's threshold T first, then the keys equal
+// to T -- each in index order, so the list is NOT in index order overall; it is in per-key index order:
+// keys of one value always fall in one class, so entries of equal value keep their index order.
+// Every element of a level's top-k is in its chunk's top-k, so the union of the chunk lists, chunks in
+// order, holds the level's top-k, and equal keys in it sit in index order (within a chunk by the rule
+// above, across chunks by chunk order): the level kernel's selection, which resolves ties at its cut by
+// list position, therefore takes the same elements as over the whole level, from at most nchunk x KC
+// entries instead of 120,000 logits per image at P2 through its five radix passes
+// (tests/test_gpu_plan_records.py: chunked and unchunked records are equal under heavy ties).
 template <int NT, int KC>
 __global__ void __launch_bounds__(NT) rpn_chunk_select_kernel(RpnParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];

@@ -553,9 +553,14 @@ static int64_t check_topology(const edgedet_op* ops, int64_t n) {
                             at + "group on a lane that is not forked");
             const int64_t kind = ops[k + 1].kind;
             EDGEDET_REQUIRE(kind == EDGEDET_OP_CONV || kind == EDGEDET_OP_DWCONV, at + "group: CONV or DWCONV members");
-            for (int64_t j = k + 1; j <= k + g; ++j)
+            for (int64_t j = k + 1; j <= k + g; ++j) {
                 EDGEDET_REQUIRE(ops[j].kind == kind && ops[j].i[EDGEDET_OP_LANE] == lane,
                                 at + "group: members of one kind on the group's lane");
+                // one grouped launch runs one tile: run_group resolves member 0's requested tile
+                // for every member, so members requesting different tiles are refused here
+                EDGEDET_REQUIRE(kind != EDGEDET_OP_CONV || ops[j].i[23] == ops[k + 1].i[23],
+                                at + "group: CONV members requesting different tiles (i23)");
+            }
             k += g;
         } else {
             const int64_t lane = o.i[EDGEDET_OP_LANE];

@@ -1222,7 +1222,7 @@ class FasterRCNN : public ResNetFPN {
   public:
     static constexpr int RPN_PRE = 1000, RPN_POST = 1000, BOX_DETS = 100;
     static constexpr int RPN_TILE = 39;  // the grouped RPN head 3x3 convs (Cout = 256): 128 x 256
-    static constexpr int RPN_CHUNK = 8192;  // anchors per chunk of the chunked RPN top-k  // the grouped RPN 3x3 convs: the P2 level's tuned tile (256 x 128)
+    static constexpr int RPN_CHUNK = 8192;  // anchors per chunk of the chunked RPN top-k
     static constexpr double RPN_NMS = 0.7, RPN_MIN = 1e-3, RPN_SCORE = 0.0, BOX_SCORE = 0.05, BOX_NMS = 0.5,
                             BOX_MIN = 1e-2;
 

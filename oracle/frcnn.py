@@ -174,7 +174,9 @@ class FasterRCNNOracle:
         x, sizes = tv_ops.transform(list(images), MEAN, STD, MIN_SIZE, MAX_SIZE, divisible=DIVISIBLE)
         feats = fpn(resnet_body(x.to(self.dtype), sd, hook), sd, hook)
         objs, dels, anchors = rpn_head(feats, sd, tuple(x.shape[-2:]))
-        props = rpn_filter([o.to(torch.float32) for o in objs], [d.to(torch.float32) for d in dels], anchors, sizes)
+        objs, dels = [o.to(torch.float32) for o in objs], [d.to(torch.float32) for d in dels]
+        self.last_rpn = (objs, dels, anchors)  # the proposal filter's inputs (end-to-end parity tests)
+        props = rpn_filter(objs, dels, anchors, sizes)
         logits, deltas = self.box_stage(feats, props, sizes, hook, sd)
         self.used_keys = sd.used
         return logits, deltas, props, sizes, feats

@@ -181,9 +181,13 @@ def _topk_before(side, st, x, y):
     return side.tkties[tie][x] < side.tkties[tie][y]
 
 
-def classify(sA, tA, sB, tB, stages):
+def classify(sA, tA, sB, tB, stages, absent=None):
     """Attribute every candidate whose fate differs between side A (oracle) and side B (engine).
-    Returns {"flips": [dict per divergent candidate], "unexplained": [ids], "by_stage": {...}}."""
+    absent = (bool [n] for A, bool [n] for B): candidates that do not exist on that side (an
+    end-to-end box stage over the union of both sides' proposals: a proposal one side's RPN did not
+    emit).  Such a candidate is dropped by the first stage (a filter) on that side, and the divergence
+    is attributed to the upstream flip ("proposal_flip"), which the caller must explain at its own
+    stage.  Returns {"flips": [dict per divergent candidate], "unexplained": [ids], "by_stage": {...}}."""
     fa, fb = tA.fate, tB.fate
     div = np.nonzero(fa != fb)[0]
     base, deps, info = {}, {}, {}
@@ -195,7 +199,10 @@ def classify(sA, tA, sB, tB, stages):
         A_passes = fa[x] > s
         P, D, tP, tD = (sA, sB, tA, tB) if A_passes else (sB, sA, tB, tA)
         rec = {"id": x, "stage": s, "kind": kind, "dropped_by": "engine" if A_passes else "oracle"}
-        if kind == "filter":
+        if absent is not None and absent[1 if A_passes else 0][x]:
+            rec.update(margin=None)
+            base[x] = "proposal_flip"
+        elif kind == "filter":
             _, name, thr, op = st
             qa, qb = float(sA.q[name][x]), float(sB.q[name][x])
             okP = (P.q[name][x] > thr) if op == ">" else (P.q[name][x] >= thr)

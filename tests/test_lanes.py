@@ -63,3 +63,14 @@ def test_bad_topologies_refused_before_issue(msg):
     L = ops.lib()
     assert L.edgedet_plan_run(r.ctypes.data_as(ctypes.c_void_p), len(r), None) < 0
     assert msg.strip() in L.edgedet_last_error().decode()
+
+
+def test_group_members_requesting_different_tiles_refused():
+    """run_group launches every CONV member with member 0's tile, so check_topology refuses a GROUP
+    whose CONV members request different tiles (i23) instead of silently running one of them."""
+    r = _recs([(ops.GROUP, 2, 0, 0), (ops.CONV, 0, 0, 0), (ops.CONV, 0, 0, 0)])
+    r[1]["i"][23], r[2]["i"][23] = 31, 31
+    assert _check(r) == 0
+    r[2]["i"][23] = 39
+    assert _check(r) < 0
+    assert "different tiles" in ops.lib().edgedet_last_error().decode()
