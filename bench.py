@@ -17,8 +17,11 @@ images are independent, no collective on the data path); the timed region is bra
 barrier + device sync and the max over ranks is taken.
 
 Extra objects on the JSON line:
-  roofline      the dominant kernel of the SSD step (by measured time): algorithmic bytes or flops
-                per launch / its average launch time (HIP events on the plan's stream)
+  roofline      the dominant kernel of the SSD step (the dominant family by solo device time, its largest
+                launch): algorithmic bytes or flops per launch / its average launch time IN THE RUNNING
+                PIPELINE (the kernel's own start / end stamps on the GPU clock, written into a probe slot
+                in every instance's captured graph: pipeline_launch_ms); the same launch timed alone
+                with HIP events is reported beside it (launch_ms_solo / frac_solo)
   cpu_baseline  the CPU oracle (a restatement of the reference's torchvision CPU path, detect.py's
                 batch=1 loop) timed on a bounded sample on this host, rank 0 only
   end_to_end    uint8 host images -> detect.py's .npy rows: pinned staging, H2D of the bytes, forward,
@@ -73,7 +76,7 @@ def step(plan, stream, d2h):
 
 
 TIMING = {}  # how the last timed_steps call measured (reported on the JSON line)
-SETTLE_S = 0.5  # untimed device warm-up before the warmup passes (seconds of wall time)
+SETTLE_S = float(os.environ.get("EDGEDET_BENCH_SETTLE", "0.5"))  # untimed device warm-up before the warmup passes (s)
 
 
 def timed_steps(plan, stream, steps, warmup, dist, extra=()):
@@ -435,7 +438,120 @@ def roofline_for(plan, stream, step_ms, model=""):
         out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4)})
     out["traffic"] = None
+    out["record"] = k
     return out
+
+
+def attach_pipeline(roof, instances, steps):
+    """The roofline launch timed in the running pipeline (pipeline_launch_ms): `launch_ms`, `achieved`
+    and `frac` become the in-pipeline figures (the kernel-trace average of the same launch is what
+    they are checked against, profiles/); the solo figures stay beside them as *_solo."""
+    res = pipeline_launch_ms(instances, roof["record"], steps)
+    if res is None:
+        roof["frac_in_pipeline"] = None
+        return
+    ms, nlaunch, ips = res
+    work = roof["algorithmic_flops"] if roof["bound"] == "mfma" else roof["algorithmic_bytes"]
+    scale = 1e12 if roof["bound"] == "mfma" else 1e9
+    roof["launch_ms_solo"], roof["achieved_solo"], roof["frac_solo"] = roof["launch_ms"], roof["achieved"], roof["frac"]
+    ach = work / (ms * 1e-3) / scale
+    roof.update({"launch_ms": round(ms, 4), "achieved": round(ach, 2), "frac": round(ach / roof["peak"], 4),
+                 "frac_in_pipeline": round(ach / roof["peak"], 4),
+                 "timing": f"first workgroup start to last workgroup end on the GPU's 100 MHz clock, written by the "
+                           f"kernel into a probe slot, {nlaunch} launches over {steps} pipelined passes of "
+                           f"{len(instances)} instances ({ips:.1f} img/s with the probes); *_solo: the launch "
+                           f"alone, HIP events around 20 back-to-back replays",
+                 "stretch_vs_solo": round(ms / roof["launch_ms_solo"], 3)})
+
+
+def _probe_records(recs, k, slot_ptr):
+    """The plan's records with the launch at record k (a GROUP record: its members, the one grouped
+    launch) carrying a timing-probe slot (CONV p9, csrc/kernels.hpp ConvParams::stamp), zeroed by a
+    MEMSET record just before it on the same lane."""
+    from edgeml_amd import ops as O
+    end = k + 1 + (int(recs[k]["i"][0]) if recs[k]["kind"] == O.GROUP else 0)
+    lane = int(recs[k]["i"][O.LANE_FIELD])
+    body = recs[k:end].copy()
+    for r in body:
+        if r["kind"] == O.CONV:
+            r["p"][9] = slot_ptr
+    z = np.zeros(1, dtype=O.OP_DTYPE)
+    z[0]["kind"] = O.MEMSET
+    z[0]["i"][0] = 16
+    z[0]["p"][0] = slot_ptr
+    z[0]["i"][O.LANE_FIELD] = lane
+    return np.ascontiguousarray(np.concatenate([recs[:k], z, body, recs[end:]]))
+
+
+def pipeline_launch_ms(instances, k, steps):
+    """Average duration (ms) of the launch at record k in the RUNNING pipeline.  Every instance's plan is
+    captured again with a timing-probe slot on that launch (_probe_records), in two variants per
+    instance (own slot each); the bf16x6 kernels write their first workgroup's start and last
+    workgroup's end on the GPU's 100 MHz constant clock into the slot (s_memrealtime, vector atomics),
+    and a 16-byte D2H copy after each pass's detections brings it to pinned host memory.  Passes are
+    issued exactly as timed_steps issues them (round robin, at most 2n outstanding, completion event
+    after each pass's D2H); a variant is reused two cycles later, after the ring has waited for its
+    previous pass, whose slot is read then.  The span includes the time the launch's workgroups wait for
+    CU slots held by the kernels of the other chains / instances running beside it: what a kernel
+    trace of the pipeline shows, and what the solo timing of per_op_times leaves out.  (HIP events
+    recorded inside a captured graph do not time: hipEventElapsedTime refuses them on this ROCm.)
+    Returns (mean ms, launches timed, img/s of these passes) or None when the launch's kernel does not
+    write the probe (only the bf16x6 conv tiles do)."""
+    import ctypes
+    from edgeml_amd import ops as O
+    L = O.lib()
+    n = len(instances)
+    slots = []
+    for p, s in instances:
+        dev = torch.zeros((2, 2), dtype=torch.int64, device="cuda")
+        host = torch.zeros((2, 2), dtype=torch.int64, pin_memory=True)
+        vs = []
+        for v in range(2):
+            recs = _probe_records(p.records, k, dev[v].data_ptr())
+            g = ctypes.c_void_p()
+            O.check(L.edgedet_graph_create(recs.ctypes.data_as(ctypes.c_void_p), len(recs), O.stream_handle(s),
+                                           ctypes.byref(g)))
+            vs.append([g, False])
+        slots.append((p, s, d2h_buffers(p), vs, dev, host))
+    ring, ticks = [], []
+
+    def read(host, v):
+        st, en = int(host[v, 0]) & 0xFFFFFFFFFFFFFFFF, int(host[v, 1]) & 0xFFFFFFFFFFFFFFFF
+        return None if not st or not en else en - ((~st) & 0xFFFFFFFFFFFFFFFF)
+
+    def issue(j, keep):
+        while len(ring) >= 2 * n:
+            ring.pop(0).synchronize()
+        p, s, d2h, vs, dev, host = slots[j % n]
+        v = (j // n) % 2
+        if vs[v][1] and keep:  # this variant's previous pass (2n passes back) has completed
+            ticks.append(read(host, v))
+        O.check(L.edgedet_graph_launch(vs[v][0], O.stream_handle(s)))
+        with torch.cuda.stream(s):
+            for d, h in d2h:
+                h.copy_(d, non_blocking=True)
+            host[v].copy_(dev[v], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(s)
+        ring.append(ev)
+        vs[v][1] = True
+        return ev
+    for j in range(4 * n):  # settle: every variant used once
+        issue(j, False)
+    first = issue(4 * n, True)
+    for j in range(4 * n + 1, 4 * n + 1 + steps):
+        last = issue(j, True)
+    torch.cuda.synchronize()
+    for _, _, _, vs, _, host in slots:
+        for v in range(2):
+            ticks.append(read(host, v))
+    ips = steps * instances[0][0].B / (first.elapsed_time(last) / 1e3)
+    for _, _, _, vs, _, _ in slots:
+        for g, _ in vs:
+            L.edgedet_graph_destroy(g)
+    if not ticks or any(t is None for t in ticks):
+        return None
+    return float(np.mean(ticks)) * 1e-5, len(ticks), ips  # 100 MHz ticks -> ms
 
 
 def launch_count(plan):
@@ -698,6 +814,10 @@ def main():
         out["ssd"] = {"value": world * B * args.steps / el, "ms_per_step": 1e3 * el / args.steps, "batch": B,
                       "inflight": nin, "dets_per_img": float(plan.out_count.tensor().float().mean().item()),
                       "timing": dict(TIMING)}
+        if rank == 0 and not args.no_roofline:
+            out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps, "ssd")
+            attach_pipeline(out["ssd"]["roofline"], [(plan, stream)] + extra, max(args.steps, 40 * nin))
+            attach_traffic(out["ssd"]["roofline"], "ssd")
         # SURVEY §8(d)'s binding roof for C2: 87.1 MB of algorithmic HBM traffic per image with the fp32
         # input image (4.92 MB); a uint8 input batch reads 1.23 MB of it instead
         bpi = SSD_BYTES_PER_IMG - (3 * 640 * 640 * 3 if u8 else 0)
@@ -711,9 +831,6 @@ def main():
             del more
             out["ssd"]["alt_inflight"] = {"inflight": alt, "value": round(world * B * args.steps / el2, 2)}
         del extra
-        if rank == 0 and not args.no_roofline:
-            out["ssd"]["roofline"] = roofline_for(plan, stream, 1e3 * el / args.steps, "ssd")
-            attach_traffic(out["ssd"]["roofline"], "ssd")
         del plan
         m.plans.clear()
         if rank == 0 and not args.no_e2e:
@@ -734,11 +851,12 @@ def main():
         steps = max(20, args.steps // 10)
         extra = inflight_instances(m, B, args.inflight or m.INFLIGHT, 100 * rank + 70, u8)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
-        del extra
         out["retinanet"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
                             "dets_per_img": float(plan.out_count.tensor().float().mean().item())}
         if rank == 0 and not args.no_roofline:
             out["retinanet"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "retinanet")
+            attach_pipeline(out["retinanet"]["roofline"], [(plan, stream)] + extra, max(steps, 8 * len(extra) + 8))
+        del extra
         del plan
     if args.model in ("frcnn", "both", "all"):
         B = args.frcnn_batch
@@ -755,7 +873,6 @@ def main():
         steps = max(20, args.steps // 10)  # FRCNN steps are ~20x SSD's: at least 20 (about half a second)
         el = timed_steps(plan, stream, steps, max(2, args.warmup // 4), dist, extra)
         timing = dict(TIMING)
-        del extra
         R = float(plan.proposal_count.tensor().float().mean().item())
         gflop = 2 * (151.45e9 + 128.92e6 * R) / 1e9
         out["frcnn"] = {"value": world * B * steps / el, "ms_per_step": 1e3 * el / steps, "batch": B,
@@ -763,7 +880,9 @@ def main():
                         "tflops_model": round(gflop * B * steps / el / 1e3 / world, 2), "timing": timing}
         if rank == 0 and not args.no_roofline:
             out["frcnn"]["roofline"] = roofline_for(plan, stream, 1e3 * el / steps, "frcnn")
+            attach_pipeline(out["frcnn"]["roofline"], [(plan, stream)] + extra, max(steps, 8 * len(extra) + 8))
             attach_traffic(out["frcnn"]["roofline"], "frcnn")
+        del extra
         del plan
         m.plans.clear()
         if rank == 0 and not args.no_e2e:

@@ -1267,17 +1267,35 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
 // over up to EDGEDET_MAX_GROUP independent problems of the same tile and template variant (e.g. the
 // twelve SSDLite head 1x1 convs), workgroup ranges [g.start[k], g.start[k+1]) running problem k with
 // its own XCD-aware block order.
+// Timing probe of a launch (ConvParams::stamp, bench.py's in-pipeline roofline; a null pointer in every
+// product plan, so the product path pays one uniform branch): the first workgroup's start and the last
+// workgroup's end on the 100 MHz constant clock, folded into the slot with vector atomics (start as
+// max of its complement, so a zeroed slot needs no initial value).
+__device__ __forceinline__ void stamp_begin(unsigned long long* st) {
+    if (st && threadIdx.x == 0) atomicMax(st, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long* st) {
+    if (st) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(st + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+}
+
 template <bool XF, bool UT, bool PS, int BM = 256, int PF = 1, bool P1 = false, int BN = 128>
 __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_kernel(ConvParams p) {
+    stamp_begin(p.stamp);
     conv_x6b_body<XF, UT, PS, BM, PF, P1, BN>(p, (int)blockIdx.x);
+    stamp_end(p.stamp);
 }
 
 template <bool XF, bool UT, int BM, bool P1, int BN>
 __global__ void __launch_bounds__(512, BM == 64 || BN == 64 ? 2 : 1) conv_x6b_group_kernel(ConvGroup g) {
     const int bx = (int)blockIdx.x;
+    stamp_begin(g.p[0].stamp);
     int k = 0;
     while (k + 1 < g.n && bx >= g.start[k + 1]) ++k;  // uniform: scalar loads of the range table
     conv_x6b_body<XF, UT, false, BM, 1, P1, BN>(g.p[k], bx - g.start[k]);
+    stamp_end(g.p[0].stamp);
 }
 
 // Pre-split of a conv input for the PS tile: out[pl][pix][c] (three dense bf16 planes, the RN split

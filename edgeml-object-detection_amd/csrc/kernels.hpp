@@ -26,6 +26,10 @@ struct ConvParams {
     int lin_x, lin_y, lin_res;  // dense-layout fast paths (set by conv_launch)
     int ksplit;                 // 2: K halves accumulated with atomics into a zeroed y (tile 26)
     FastDiv div_howo, div_wo, div_cin, div_kw;
+    // timing probe (bench.py's in-pipeline roofline; null in every product plan): the bf16x6 kernels
+    // record their first workgroup's start and last workgroup's end on the 100 MHz constant clock,
+    // stamp[0] = max(~start) and stamp[1] = max(end), into a zeroed 16-byte slot (CONV record p9)
+    unsigned long long* stamp;
 };
 
 // Up to EDGEDET_MAX_GROUP conv problems issued as one launch (conv_group_launch): problem k runs the

@@ -922,7 +922,9 @@ class SSDLite {
             P.add(o);
         }
         const int64_t NS = NC - 1, KM = TOPK;
-        if (NS * KM <= 512 * 54 && DETS <= 1024) {
+        // EDGEDET_SSD_NMS=class: per-(image, class) NMS on every class's top-k, then the per-image merge
+        // (the form the image-greedy kernel replaced; an A/B switch)
+        if (NS * KM <= 512 * 54 && DETS <= 1024 && !env_is("EDGEDET_SSD_NMS", "class", "image")) {
             const int pk = P.buf({B, NS, KM}, I32, "pool.key" + sfx);
             const int pr = P.buf({B, NS, KM}, I32, "pool.ref" + sfx);
             OpRec o;
