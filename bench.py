@@ -104,8 +104,10 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     the issue discipline and fresh per-model streams (main) remove both.  Every instance was primed
     when it was captured (graph uploaded and replayed, plan.capture), and the warmup covers each
     instance at least once.  The ranks start together (barrier + device sync before the warmup) and
-    end together (device sync + barrier after the last pass); the max over ranks is taken.  The host wall clock of the K timed passes (from the
-    first timed issue to the final sync, so it includes the drain) is kept in TIMING."""
+    end together (device sync + barrier after the last pass); the max over ranks is taken.  After the K
+    timed passes 2n more passes are issued untimed (a full pipeline at the end of the window too, as at
+    its start).  The host wall clock of the K timed passes (from the first timed issue to the last timed
+    pass's completion) is kept in TIMING."""
     lanes = [(p, s, d2h_buffers(p)) for p, s in [(plan, stream)] + list(extra)]
     n = len(lanes)
     warm = max(warmup, n)
@@ -145,10 +147,18 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
     t0 = time.perf_counter()
     for i in range(steps):
         done.append(issue(settled + warm + i, timing=True))
+    # tail: 2n more passes, untimed, so the last timed passes complete under the contention of the
+    # passes behind them, as every pass of a long run does.  Without them the pipeline drains at the
+    # end of the window: the last passes run with nothing queued behind them and finish early, which
+    # read a 20-pass window 1-3 % above the steady rate (profiles/r5c_bias.txt; a 3,000-pass trace is
+    # flat, and its 20-pass windows scatter by 0.8 %).
+    for i in range(2 * n):
+        issue(settled + warm + steps + i)
+    done[-1].synchronize()
+    wall = time.perf_counter() - t0
     for _, s, _ in lanes:
         s.synchronize()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
     el = mark.elapsed_time(done[-1]) / 1e3 * steps / (steps + r)
     if os.environ.get("EDGEDET_BENCH_TRACE"):  # per-pass completion times (timing investigation)
         with open(os.environ["EDGEDET_BENCH_TRACE"], "a") as fh:
@@ -163,9 +173,10 @@ def timed_steps(plan, stream, steps, warmup, dist, extra=()):
         el, wall = (float(v) for v in t.tolist())
     TIMING.clear()
     TIMING.update({"method": "steady state: HIP completion events after each pass's D2H, pipeline kept full "
-                             "across the start; interval between two completions of the same instance "
-                             "(K + r passes, r = (-K) mod instances), scaled to K",
-                   "device_s": round(el, 6), "interval_passes": steps + r, "wall_s_incl_drain": round(wall, 6),
+                             "across the start and the end (2n untimed tail passes); interval between two "
+                             "completions of the same instance (K + r passes, r = (-K) mod instances), "
+                             "scaled to K",
+                   "device_s": round(el, 6), "interval_passes": steps + r, "wall_s": round(wall, 6),
                    "warmup_passes": warm, "settle_passes": settled, "instances": n})
     return el
 
@@ -457,8 +468,8 @@ def attach_pipeline(roof, instances, steps):
     ach = work / (ms * 1e-3) / scale
     roof.update({"launch_ms": round(ms, 4), "achieved": round(ach, 2), "frac": round(ach / roof["peak"], 4),
                  "frac_in_pipeline": round(ach / roof["peak"], 4),
-                 "timing": f"first workgroup start to last workgroup end on the GPU's 100 MHz clock, written by the "
-                           f"kernel into a probe slot, {nlaunch} launches over {steps} pipelined passes of "
+                 "timing": f"workgroup 0's start to the last workgroup's end on the GPU's 100 MHz clock, written by "
+                           f"the kernel into a probe slot, {nlaunch} launches over {steps} pipelined passes of "
                            f"{len(instances)} instances ({ips:.1f} img/s with the probes); *_solo: the launch "
                            f"alone, HIP events around 20 back-to-back replays",
                  "stretch_vs_solo": round(ms / roof["launch_ms_solo"], 3)})
@@ -466,89 +477,85 @@ def attach_pipeline(roof, instances, steps):
 
 def _probe_records(recs, k, slot_ptr):
     """The plan's records with the launch at record k (a GROUP record: its members, the one grouped
-    launch) carrying a timing-probe slot (CONV p9, csrc/kernels.hpp ConvParams::stamp), zeroed by a
-    MEMSET record just before it on the same lane."""
+    launch) carrying a timing-probe slot (CONV p9, csrc/kernels.hpp ConvParams::stamp); nothing else
+    changes (no extra record: the slot needs no reset between launches)."""
     from edgeml_amd import ops as O
     end = k + 1 + (int(recs[k]["i"][0]) if recs[k]["kind"] == O.GROUP else 0)
-    lane = int(recs[k]["i"][O.LANE_FIELD])
-    body = recs[k:end].copy()
-    for r in body:
+    out = np.ascontiguousarray(recs.copy())
+    for r in out[k:end]:
         if r["kind"] == O.CONV:
             r["p"][9] = slot_ptr
-    z = np.zeros(1, dtype=O.OP_DTYPE)
-    z[0]["kind"] = O.MEMSET
-    z[0]["i"][0] = 16
-    z[0]["p"][0] = slot_ptr
-    z[0]["i"][O.LANE_FIELD] = lane
-    return np.ascontiguousarray(np.concatenate([recs[:k], z, body, recs[end:]]))
+    return out
 
 
 def pipeline_launch_ms(instances, k, steps):
     """Average duration (ms) of the launch at record k in the RUNNING pipeline.  Every instance's plan is
-    captured again with a timing-probe slot on that launch (_probe_records), in two variants per
-    instance (own slot each); the bf16x6 kernels write their first workgroup's start and last
-    workgroup's end on the GPU's 100 MHz constant clock into the slot (s_memrealtime, vector atomics),
-    and a 16-byte D2H copy after each pass's detections brings it to pinned host memory.  Passes are
-    issued exactly as timed_steps issues them (round robin, at most 2n outstanding, completion event
-    after each pass's D2H); a variant is reused two cycles later, after the ring has waited for its
-    previous pass, whose slot is read then.  The span includes the time the launch's workgroups wait for
-    CU slots held by the kernels of the other chains / instances running beside it: what a kernel
-    trace of the pipeline shows, and what the solo timing of per_op_times leaves out.  (HIP events
-    recorded inside a captured graph do not time: hipEventElapsedTime refuses them on this ROCm.)
-    Returns (mean ms, launches timed, img/s of these passes) or None when the launch's kernel does not
-    write the probe (only the bf16x6 conv tiles do)."""
+    captured again with a timing-probe slot on that launch (_probe_records; the same records otherwise)
+    and primed like plan.capture; the bf16x6 kernels write workgroup 0's start and the last workgroup's
+    end on the GPU's 100 MHz constant clock into the slot (s_memrealtime, vector atomics), and a 16-byte
+    D2H copy after each pass's detections brings it to pinned host memory (two host buffers per
+    instance, alternating, so a buffer is read after the ring has waited for its pass, two cycles
+    back).  Settle and passes are issued exactly as timed_steps issues them (round robin, at most 2n
+    outstanding, completion event after each pass's D2H).  The span includes the time the launch's
+    workgroups wait for CU slots held by the kernels of the other chains / instances running beside
+    it: what a kernel trace of the pipeline shows, and what the solo timing of per_op_times leaves
+    out.  (HIP events recorded inside a captured graph do not time: hipEventElapsedTime refuses them
+    on this ROCm.)  Returns (mean ms, launches timed, img/s of these passes), or None when the
+    launch's kernel does not write the probe (only the bf16x6 conv tiles do)."""
     import ctypes
     from edgeml_amd import ops as O
     L = O.lib()
     n = len(instances)
     slots = []
     for p, s in instances:
-        dev = torch.zeros((2, 2), dtype=torch.int64, device="cuda")
+        dev = torch.zeros(2, dtype=torch.int64, device="cuda")
         host = torch.zeros((2, 2), dtype=torch.int64, pin_memory=True)
-        vs = []
-        for v in range(2):
-            recs = _probe_records(p.records, k, dev[v].data_ptr())
-            g = ctypes.c_void_p()
-            O.check(L.edgedet_graph_create(recs.ctypes.data_as(ctypes.c_void_p), len(recs), O.stream_handle(s),
-                                           ctypes.byref(g)))
-            vs.append([g, False])
-        slots.append((p, s, d2h_buffers(p), vs, dev, host))
+        recs = _probe_records(p.records, k, dev.data_ptr())
+        g = ctypes.c_void_p()
+        O.check(L.edgedet_graph_create(recs.ctypes.data_as(ctypes.c_void_p), len(recs), O.stream_handle(s),
+                                       ctypes.byref(g)))
+        for _ in range(2):  # prime, as plan.capture does
+            O.check(L.edgedet_graph_launch(g, O.stream_handle(s)))
+        slots.append((p, s, d2h_buffers(p), g, dev, host, [False, False]))
+    torch.cuda.synchronize()
     ring, ticks = [], []
 
     def read(host, v):
-        st, en = int(host[v, 0]) & 0xFFFFFFFFFFFFFFFF, int(host[v, 1]) & 0xFFFFFFFFFFFFFFFF
-        return None if not st or not en else en - ((~st) & 0xFFFFFFFFFFFFFFFF)
+        st, en = int(host[v, 0]), int(host[v, 1])
+        return en - st if st and en > st else None
 
     def issue(j, keep):
         while len(ring) >= 2 * n:
             ring.pop(0).synchronize()
-        p, s, d2h, vs, dev, host = slots[j % n]
+        p, s, d2h, g, dev, host, used = slots[j % n]
         v = (j // n) % 2
-        if vs[v][1] and keep:  # this variant's previous pass (2n passes back) has completed
+        if used[v] and keep:  # this buffer's pass (2n passes back) has completed
             ticks.append(read(host, v))
-        O.check(L.edgedet_graph_launch(vs[v][0], O.stream_handle(s)))
+        O.check(L.edgedet_graph_launch(g, O.stream_handle(s)))
         with torch.cuda.stream(s):
             for d, h in d2h:
                 h.copy_(d, non_blocking=True)
-            host[v].copy_(dev[v], non_blocking=True)
+            host[v].copy_(dev, non_blocking=True)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(s)
         ring.append(ev)
-        vs[v][1] = True
+        used[v] = True
         return ev
-    for j in range(4 * n):  # settle: every variant used once
+    t0, j = time.perf_counter(), 0
+    while time.perf_counter() - t0 < SETTLE_S or j < 4 * n:  # settle, as timed_steps
         issue(j, False)
-    first = issue(4 * n, True)
-    for j in range(4 * n + 1, 4 * n + 1 + steps):
-        last = issue(j, True)
+        j += 1
+    first = issue(j, True)
+    for j2 in range(j + 1, j + 1 + steps):
+        last = issue(j2, True)
     torch.cuda.synchronize()
-    for _, _, _, vs, _, host in slots:
+    for _, _, _, _, _, host, used in slots:
         for v in range(2):
-            ticks.append(read(host, v))
+            if used[v]:
+                ticks.append(read(host, v))
     ips = steps * instances[0][0].B / (first.elapsed_time(last) / 1e3)
-    for _, _, _, vs, _, _ in slots:
-        for g, _ in vs:
-            L.edgedet_graph_destroy(g)
+    for sl in slots:
+        L.edgedet_graph_destroy(sl[3])
     if not ticks or any(t is None for t in ticks):
         return None
     return float(np.mean(ticks)) * 1e-5, len(ticks), ips  # 100 MHz ticks -> ms

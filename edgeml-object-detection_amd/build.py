@@ -61,20 +61,25 @@ def up_to_date():
 DIAG_LIB = os.path.join(HERE, "libedgedet_diag.so")
 
 
-def build(force=False, verbose=False, jobs=8, diag=False):
+def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=()):
     """diag=True: libedgedet_diag.so with -DEDGEDET_DIAG (the EDGEDET_DIAG_SKIP op-family skips of
-    csrc/exec.hip, wrong results; load it with EDGEDET_LIB, tools/gpu_skip.sh).  Never the product."""
-    lib = DIAG_LIB if diag else LIB
+    csrc/exec.hip, wrong results; load it with EDGEDET_LIB, tools/gpu_skip.sh).  variant="name" with
+    defines=("NMS_PROFILE", ...): libedgedet_<name>.so built with those -D flags (diagnostic builds,
+    loaded with EDGEDET_LIB).  Never the product."""
+    if variant:
+        diag = True
+    lib = os.path.join(HERE, f"libedgedet_{variant}.so") if variant else (DIAG_LIB if diag else LIB)
     if not force and not diag and up_to_date():
         return LIB
     cc = hipcc()
-    objdir = os.path.join(HERE, "build_diag" if diag else "build")
+    objdir = os.path.join(HERE, f"build_{variant}" if variant else ("build_diag" if diag else "build"))
     os.makedirs(objdir, exist_ok=True)
     write_tile_table(objdir)
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
-        cmd = [cc, *FLAGS, *(["-DEDGEDET_DIAG"] if diag else []), "-I", objdir, "-c", src, "-o", obj]
+        dflags = [f"-D{d}" for d in defines] if variant else (["-DEDGEDET_DIAG"] if diag else [])
+        cmd = [cc, *FLAGS, *dflags, "-I", objdir, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -1268,11 +1268,14 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
 // twelve SSDLite head 1x1 convs), workgroup ranges [g.start[k], g.start[k+1]) running problem k with
 // its own XCD-aware block order.
 // Timing probe of a launch (ConvParams::stamp, bench.py's in-pipeline roofline; a null pointer in every
-// product plan, so the product path pays one uniform branch): the first workgroup's start and the last
-// workgroup's end on the 100 MHz constant clock, folded into the slot with vector atomics (start as
-// max of its complement, so a zeroed slot needs no initial value).
+// product plan, so the product path pays one uniform branch), on the 100 MHz constant clock with vector
+// atomics: stamp[0] = the start of workgroup 0 (workgroups are dispatched in id order, so it is the
+// first to start), stamp[1] = max of every workgroup's end.  The clock only grows and one slot serves
+// one stream's launches in order, so the slot needs no reset between launches: stamp[1] - stamp[0]
+// after a launch is that launch's span.
 __device__ __forceinline__ void stamp_begin(unsigned long long* st) {
-    if (st && threadIdx.x == 0) atomicMax(st, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (st && threadIdx.x == 0 && blockIdx.x == 0)
+        atomicExch(st, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 __device__ __forceinline__ void stamp_end(unsigned long long* st) {
     if (st) {

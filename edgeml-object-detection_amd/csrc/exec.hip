@@ -15,7 +15,7 @@
 //                  i0..11 B,H,W,Cin,Ho,Wo,Cout,KH,KW,stride,pad,act; i12 K; i13 Kpad;
 //                  i14..16 x/y/res pixel strides; i17..19 x/y/res batch strides; i20 y offset;
 //                  i21..22 res_H,res_W (nearest upsample source, 0 = same); i23 tile (0 = auto);
-//                  p9 timing probe slot (2 x u64, zeroed; bf16x6 tiles only; 0 in product plans)
+//                  p9 timing probe slot (2 x u64; bf16x6 tiles only; 0 in product plans)
 //   SSD_STEM       p0 x NHWC4; p1 w0 [16][i5]; p2 b0; p3 wd [9][16]; p4 bd; p5 w1 [16][i6]; p6 b1; p7 y;
 //                  i0..4 B,H,W,Ho,Wo (SSDLite features.0.0 + features.0.1 fused)
 //   DWCONV         p0 x; p1 w[K*K][C]; p2 bias; p3 y; p4 SE partial sums [B,16,C] | 0;

@@ -27,8 +27,8 @@ struct ConvParams {
     int ksplit;                 // 2: K halves accumulated with atomics into a zeroed y (tile 26)
     FastDiv div_howo, div_wo, div_cin, div_kw;
     // timing probe (bench.py's in-pipeline roofline; null in every product plan): the bf16x6 kernels
-    // record their first workgroup's start and last workgroup's end on the 100 MHz constant clock,
-    // stamp[0] = max(~start) and stamp[1] = max(end), into a zeroed 16-byte slot (CONV record p9)
+    // record workgroup 0's start (stamp[0]) and the max of every workgroup's end (stamp[1]) on the
+    // 100 MHz constant clock into a 16-byte slot (CONV record p9)
     unsigned long long* stamp;
 };
 

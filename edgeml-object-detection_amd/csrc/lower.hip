@@ -303,6 +303,11 @@ struct External {
     }
 };
 
+// Redzone (diagnostic, edgedet_set_redzone; 0 in production): bytes left unused before the first
+// workspace buffer, between consecutive buffers and after the last, so a test can fill them with a
+// canary and find any kernel that writes outside its buffers.
+static int64_t g_redzone = 0;
+
 struct Plan {
     std::shared_ptr<const std::vector<edgedet_op>> resolved;  // records of the last forward's pointers
     External resolved_for;
@@ -400,10 +405,11 @@ struct Plan {
         forked = 0;
     }
     void finalize() {
-        int64_t off = 0;
+        const int64_t rz = g_redzone;
+        int64_t off = rz;
         for (auto& b : bufs) {
             b.off = off;
-            off += (b.nbytes + 255) / 256 * 256;
+            off += (b.nbytes + 255) / 256 * 256 + rz;
         }
         arena = off > 256 ? off : 256;
     }
@@ -1875,6 +1881,14 @@ static int config_of(int32_t kind, int32_t num_classes, int32_t reduced_tail, Co
 
 static int shape_ok(int32_t B, int32_t H, int32_t W) {
     EDGEDET_REQUIRE(B >= 1 && B <= 4096 && H >= 1 && W >= 1 && H <= 16384 && W <= 16384, "bad (B, H, W)");
+    return 0;
+}
+
+extern "C" int edgedet_set_redzone(int64_t bytes) {
+    EDGEDET_REQUIRE(bytes >= 0 && bytes % 256 == 0 && bytes <= (64 << 20), "set_redzone: 0..64 MiB, multiple of 256");
+    std::lock_guard<std::mutex> g(g_mu);
+    g_redzone = bytes;
+    for (auto& kv : g_engines) kv.second->plans.clear();  // every later lowering lays out with the new gaps
     return 0;
 }
 

@@ -46,6 +46,7 @@ OP_DTYPE = np.dtype([("kind", "<i8"), ("i", "<i8", OP_INTS), ("p", "<u8", OP_PTR
 assert OP_DTYPE.itemsize == 8 + 8 * OP_INTS + 8 * OP_PTRS + 8 * OP_DBLS + 4 * OP_FLTS
 
 EXPORTS = ("edgedet_plan_run", "edgedet_graph_create", "edgedet_graph_launch", "edgedet_graph_destroy",
+           "edgedet_set_redzone",
            "edgedet_nms", "edgedet_batched_nms", "edgedet_roi_align", "edgedet_conv2d", "edgedet_conv_weight_k",
            "edgedet_dwconv2d", "edgedet_last_error", "edgedet_version", "edgedet_target", "edgedet_conv2d_ex",
            "edgedet_split_bf16x3", "edgedet_conv_tile", "edgedet_box_correct", "edgedet_orie_ap",
@@ -92,6 +93,7 @@ def lib():
     L.edgedet_graph_create.argtypes = [_vp, _i64, _vp, ctypes.POINTER(_vp)]
     L.edgedet_graph_launch.argtypes = [_vp, _vp]
     L.edgedet_graph_destroy.argtypes = [_vp]
+    L.edgedet_set_redzone.argtypes = [_i64]
     L.edgedet_nms.argtypes = [_vp, _vp, _i64, _dbl, _vp, _vp, _vp]
     L.edgedet_batched_nms.argtypes = [_vp, _vp, _vp, _i64, _dbl, _vp, _vp, _vp]
     L.edgedet_nms_workspace_size.argtypes = [_i64]

@@ -104,6 +104,12 @@ int edgedet_graph_create(const edgedet_op* ops, int64_t n, void* stream, void** 
 int edgedet_graph_launch(void* graph, void* stream);
 int edgedet_graph_destroy(void* graph);
 
+/* Diagnostic: leave `bytes` (a multiple of 256, 0 = none, the default) unused before, between and after
+ * the workspace buffers of every plan lowered from now on (cached lowerings are dropped), so a caller
+ * can fill the gaps with a canary and catch a kernel writing outside its buffers
+ * (tests/test_gpu_redzone.py). */
+int edgedet_set_redzone(int64_t bytes);
+
 /* ------------------------------------------------------------------------ model forward */
 /*
  * The detector call of torch_models/detect.py:78 (model(images) -> boxes / scores / labels for the
