@@ -126,6 +126,19 @@ def _proposal_shift(A, B, ja, jb, c, tol):
             "response": abs(s_ab - float(A["scores"][ja, c]))}
 
 
+def _beyond_band(r, sA, tol):
+    """A base-explained witness whose reference-side margin lies outside its noise band."""
+    m = r.get("margin")
+    if m is None:
+        return False
+    if r["kind"] == "filter" and r.get("quantity") == "minsize":
+        b = sA.box[r["id"]].astype(np.float64)
+        return m / max(1.0, float(np.abs(b).max()), float(b[2] - b[0]), float(b[3] - b[1])) > EPS_SIZE
+    if r["reason"] == "iou_straddle":
+        return m > EPS_IOU
+    return m > tol
+
+
 def _filter_margins(rep, sA):
     """(largest score-filter margin, largest remove_small margin relative to the box's scale) over the
     base-explained filter straddles of a classify report."""
@@ -201,11 +214,25 @@ def check_image(A, B, NC, scale, orig_hw, own_check_A=True, tol=TOL):
     for r in brep["flips"]:
         if r["reason"] == "proposal_flip" and int(U[r["id"] // C]) not in rpn_div:
             fails.append(("proposal flip without an RPN witness", r))
+    # a box-stage witness whose reference margin lies outside its band is re-examined at the engine's
+    # proposal: the reference's box stage fed the engine's proposal must land within tol of the engine
+    # for every class that flipped on that anchor (the divergence is the proposal shift, see
+    # _proposal_shift); otherwise the flip fails
+    shifted = {}
+    for r in brep["flips"]:
+        if r["reason"] in (None, "proposal_flip", "cascade") or not _beyond_band(r, bA, tol):
+            continue
+        x = int(r["id"])
+        w = _proposal_shift(A, B, posA[x // C], posB[x // C], x % C + 1, tol)
+        if w is None:
+            fails.append(("box flip beyond its band without a witness", {k: r.get(k) for k in
+                                                                           ("id", "kind", "reason", "margin")}))
+        else:
+            r["reason"] = "proposal_shift"
+            shifted[x] = w
     b_s, b_z = _filter_margins(brep, bA)
     b_s = max(b_s, max_margin(brep, kinds=("inversion",)))
     b_i = max_margin(brep, kinds=("iou_straddle",))
-    if b_s > tol or b_i > EPS_IOU or b_z > EPS_SIZE:
-        fails.append(("box margins", b_s, b_i, b_z, brep["by_stage"]))
     box_div = {int(r["id"]) for r in brep["flips"] if r["reason"] is not None}
 
     # ---------------------------------------------------------------- identity-paired rows
@@ -258,10 +285,22 @@ def check_image(A, B, NC, scale, orig_hw, own_check_A=True, tol=TOL):
             fails.append(("rowpair pair beyond 1e-3 not attributed", {"ref_id": a, "eng_id": b, "dconf": float(d)}))
     un_ids = [int(idA[k]) for k in range(len(rA)) if not any(k == i for i, _ in pairs)] + \
              [int(idB[k]) for k in range(len(rB)) if not any(k == j for _, j in pairs)]
+    rp["unpaired_identity"] = []
     for x in un_ids:
         if x in box_div:
             rp["unpaired_flip"] += 1
-        elif x not in ok_pair and x not in lvl_ids and x not in shift_ids:
+        elif x in ok_pair:
+            # the same detection on both sides within tolerance that the IoU >= 0.99 pairing misses: a
+            # thin box, where a coordinate difference well inside 1e-3 of its size moves the IoU under 0.99
+            a, b = bA.box[x].astype(np.float64), bB.box[x].astype(np.float64)
+            iw = max(0.0, min(a[2], b[2]) - max(a[0], b[0]))
+            ih = max(0.0, min(a[3], b[3]) - max(a[1], b[1]))
+            ar = lambda q: (q[2] - q[0]) * (q[3] - q[1])  # noqa: E731
+            iou = iw * ih / (ar(a) + ar(b) - iw * ih) if ar(a) + ar(b) > 0 else 0.0
+            rp["unpaired_identity"].append({"id": x, "score": float(bA.score[x]), "iou": round(float(iou), 5),
+                                            "w": round(float(a[2] - a[0]), 3), "h": round(float(a[3] - a[1]), 3),
+                                            "dbox": float(box_rel_err(a[None], b[None])[0])})
+        elif x not in lvl_ids and x not in shift_ids:
             fails.append(("rowpair-unpaired row without a witness", x))
     rep = {"rpn_flips": len(rrep["flips"]), "rpn_by": rrep["by_stage"], "box_flips": len(brep["flips"]),
            "box_by": brep["by_stage"], "proposals_only_ref": int(len(np.setdiff1d(tA.out, tB.out))),
@@ -269,6 +308,7 @@ def check_image(A, B, NC, scale, orig_hw, own_check_A=True, tol=TOL):
            "max_identity_dscore": float(ds.max()) if len(ds) else 0.0,
            "max_identity_dbox": float(db.max()) if len(db) else 0.0,
            "level_straddles": int(level_straddle.sum()), "proposal_shifts": len(shifts),
+           "box_flips_proposal_shift": len(shifted),
            "max_shift_response": max([r["response"] for r in shifts], default=0.0),
            "max_shift_box_arith": max([r["box_stage_dscore"] for r in shifts], default=0.0),
            "max_margin": {"rpn_score": m_s, "rpn_logit": m_k, "rpn_iou": m_i, "rpn_size": m_z, "box_score": b_s,
@@ -287,6 +327,8 @@ def merge(reports):
                 for kk, vv in v.items():
                     if isinstance(vv, float):
                         d[kk] = max(d.get(kk, 0.0), vv)
+                    elif isinstance(vv, list):
+                        d[kk] = d.get(kk, []) + vv
                     else:
                         d[kk] = d.get(kk, 0) + vv
             elif isinstance(v, float):
