@@ -113,6 +113,9 @@ def _exact(kind, i, f):
             return 0, 4 * B * 3 * H0 * W0
         if f == 9:
             return 0, B * 3 * H0 * W0
+    if kind == ops.BOX_SCORES and f == 0:  # predictor rows of LD floats, 5 * NC of them written / read
+        LD, B, R, NC = i[0:4]
+        return [(4 * r * LD, 4 * 5 * NC) for r in range(B * R)]
     if kind == ops.PREPROCESS:
         B, H, W_, Ho, Wo, Hp, Wp = i[0:7]
         return {0: (0, 4 * B * 3 * H * W_), 2: (0, B * 3 * H * W_), 1: (0, 16 * B * Hp * Wp)}[f]
@@ -231,3 +234,83 @@ def check(plan, names=None):
             races.append(f"{names[pk]} on lane {plane} is not joined into lane 0 by the end of the plan")
             break
     return races
+
+
+def _subtract(lo, hi, covered):
+    """[lo, hi) minus the union of the sorted, merged intervals `covered` -> list of intervals."""
+    out, cur = [], lo
+    for a, b in covered:
+        if b <= cur:
+            continue
+        if a >= hi:
+            break
+        if a > cur:
+            out.append((cur, min(a, hi)))
+        cur = max(cur, b)
+        if cur >= hi:
+            break
+    if cur < hi:
+        out.append((cur, hi))
+    return out
+
+
+def _add(covered, lo, hi):
+    """Insert [lo, hi) into the sorted, merged interval list."""
+    res, placed = [], False
+    for a, b in covered:
+        if b < lo or a > hi:
+            res.append((a, b))
+        else:
+            lo, hi = min(lo, a), max(hi, b)
+    res.append((lo, hi))
+    res.sort()
+    return res
+
+
+def stale_reads(plan, names=None):
+    """Reads of bytes no earlier record of the same pass wrote (in issue order), classified: bytes that a
+    LATER record writes are read from the previous pass (a replayed plan would see the last pass's
+    values there, its first pass the zeroed workspace) -- reported; bytes no record writes must be the
+    constants edgedet_model_prepare wrote or the input images -- others are reported too.  Empty when
+    every read sees this pass's data or a constant."""
+    recs = plan.records
+    names = names or [op.name for op in plan.ops]
+    acc = Accesses(plan)
+    order = []  # (record index, lo, hi, role)
+    k = 0
+    while k < len(recs):
+        kind = int(recs[k]["kind"])
+        if kind in (ops.FORK, ops.JOIN, ops.WAIT):
+            k += 1
+            continue
+        members = list(range(k + 1, k + 1 + int(recs[k]["i"][0]))) if kind == ops.GROUP else [k]
+        for m in members:
+            for lo, hi, role, f in acc.ranges(recs[m]):
+                order.append((m, lo, hi, role, f))
+        k = members[-1] + 1
+    # bytes of a buffer that no record writes at all are constants (edgedet_model_prepare's anchors,
+    # the packed tables) or the caller's input images
+    written_ever = []
+    for _, lo, hi, role, _ in order:
+        if role != R:
+            written_ever = _add(written_ever, lo, hi)
+    never = []
+    for b in plan.buffers.values():
+        if not any(lo < b.off + b.nbytes and b.off < hi for lo, hi in written_ever):
+            never = _add(never, b.off, b.off + b.nbytes)
+    issues = []
+    written = []
+    for pos, (m, lo, hi, role, f) in enumerate(order):
+        if role == R:
+            for a, b in _subtract(lo, hi, written):
+                later = [(m2, max(a, l2), min(b, h2)) for (m2, l2, h2, r2, _) in order[pos + 1:]
+                         if r2 != R and l2 < b and a < h2]
+                if later:
+                    issues.append(f"{names[m]} (p{f}) reads bytes [{a}, {b}) that {names[later[0][0]]} writes later "
+                                  f"in the pass: the previous pass's values")
+                elif _subtract(a, b, never):
+                    issues.append(f"{names[m]} (p{f}) reads bytes [{a}, {b}) that no record writes, inside a "
+                                  f"buffer that records do write: uninitialised")
+        else:
+            written = _add(written, lo, hi)
+    return issues

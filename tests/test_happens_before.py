@@ -84,3 +84,25 @@ def test_checker_catches_a_dropped_wait():
     recs = plan.records[keep]
     names = [plan.ops[k].name for k in keep]
     assert joins and hb.check(_Mut(plan, recs, names))
+
+
+@pytest.mark.parametrize("kind,B,H,W,u8", CASES)
+def test_every_read_sees_this_pass_or_a_constant(kind, B, H, W, u8):
+    """No record reads bytes that only a later record of the pass writes (a replayed graph would hand
+    it the previous pass's values -- a cross-pass dependence that timing cannot disturb but that makes
+    the first pass differ from the rest), nor bytes of a written buffer that nothing writes."""
+    plan = _model(kind).build_plan(B, H, W, u8)
+    stale = hb.stale_reads(plan)
+    assert not stale, stale[:10]
+
+
+def test_stale_read_check_catches_a_consumer_moved_before_its_producer():
+    plan = _ssd32()
+    recs = plan.records
+    k = next(j for j, r in enumerate(recs) if r["kind"] == ops.CONV and j > 0 and recs[j - 1]["kind"] == ops.CONV
+             and recs[j - 1]["p"][3] == recs[j]["p"][0])
+    order = list(range(len(recs)))
+    order[k - 1], order[k] = k, k - 1
+    mut = _Mut(plan, recs[order], [plan.ops[j].name for j in order])
+    stale = hb.stale_reads(mut)
+    assert any("writes later" in s for s in stale), stale[:3]
