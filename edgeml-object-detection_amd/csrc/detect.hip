@@ -530,6 +530,50 @@ __device__ void bitonic_desc(unsigned long long* keys, int* payload, int m) {
     }
 }
 
+// Sort of keys[0..m) descending for m <= NT, one key per thread, two barriers: each wave ranks its 64
+// keys among themselves (a readlane walk: keys greater, equal keys at lower lanes first) and writes its
+// run sorted into run[]; a key's final position is its rank in its own run plus, for every other run, the
+// number of that run's keys ahead of it (binary search; equal keys: the earlier run first).  Keys past m
+// are zeros and sort last.  Replaces the 45 barrier stages of a 512-key bitonic sort.
+template <int NT>
+__device__ void rank_sort_desc(unsigned long long* keys, unsigned long long* run, int m) {
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long k = tid < m ? keys[tid] : 0ull;
+    int r = 0;
+    if (64 * w < m) {  // wave-uniform: waves wholly past m write zeros below
+        const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+#pragma unroll 16
+        for (int j = 0; j < 64; ++j) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)khi, j);
+            const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
+            r += (kj > k || (kj == k && j < lane)) ? 1 : 0;
+        }
+    } else {
+        r = lane;
+    }
+    run[64 * w + r] = k;
+    __syncthreads();
+    int pos = r;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+        if (v == w || 64 * v >= m) continue;  // a run wholly past m holds only zeros, after every key
+        const unsigned long long* rv = run + 64 * v;
+        int lo = 0;
+#pragma unroll
+        for (int st = 64; st >= 1; st >>= 1) {
+            if (lo + st <= 64) {
+                const unsigned long long e = rv[lo + st - 1];
+                if (e > k || (e == k && v < w)) lo += st;
+            }
+        }
+        pos += lo;
+    }
+    if (tid < m) keys[pos] = k;
+    __syncthreads();
+}
+
 // IoU threshold test, bit-exact with torchvision's CPU nms: `(double)RN_f32(inter / uni) > thr`, where
 // inter and uni = (area_i + area_j) - inter are computed in float in the reference's op order.  The
 // float division is replaced by an exact comparison: with t1 = the smallest float > thr and t0 its
@@ -871,6 +915,8 @@ struct ImgSmem {
     int bucket[M];        // sorted positions grouped by class, score order within a class
     unsigned long long row[M];  // per candidate: later members of its class it suppresses (bit = rank)
     int rank[M];          // rank of the candidate within its class bucket
+    unsigned long long run[M];          // rank_sort_desc's sorted 64-key runs
+    int wcnt[M / 64][SSD_MAXNC];        // per wave of sorted order: candidates of each class
     uint32_t done[PW];
     int wsum[32];
     int red[32];
@@ -929,7 +975,6 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
         const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red, false, 3 * M / 4, &nleft);
         NMS_STAMP(t_sel);
         if (m == 0) break;
-        for (int t = tid; t < NS; t += NT) S.hist[t] = 0;
         if (tid < m) {
             const int i = key_index(S.keys[tid]);
             atomicOr(&S.done[i >> 5], 1u << (i & 31));
@@ -940,15 +985,37 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             const int i = tid + NT * j;
             if (kr[j] && ((S.done[i >> 5] >> (i & 31)) & 1u)) kr[j] = 0u;
         }
-        bitonic_desc<NT>(S.keys, nullptr, m);
+        rank_sort_desc<NT>(S.keys, S.run, m);
         NMS_STAMP(t_sort);
+        // each candidate's class and its rank among the earlier sorted candidates of its class: within
+        // the wave by a ballot per distinct class (ordered by lane), across waves by the per-wave class
+        // counts; the class histogram is their sum
+        for (int t = tid; t < NW * NS; t += NT) S.wcnt[t / NS][t % NS] = 0;
+        int c = -1, rin = 0;
         if (tid < m) {
             const int i = key_index(S.keys[tid]);
-            const int c = i / topk;
+            c = i / topk;
             S.box[tid] = bx[pr[i]];
             S.cls[tid] = c;
             S.kflag[tid] = 0;
-            atomicAdd(&S.hist[c], 1);
+        }
+        __syncthreads();
+        {
+            unsigned long long todo = __ballot(c >= 0);
+            while (todo) {
+                const int leader = __ffsll((long long)todo) - 1;
+                const int cl = __builtin_amdgcn_readlane(c, leader);
+                const unsigned long long mm = __ballot(c == cl);
+                if (c == cl) rin = __popcll(mm & lt_mask);
+                if (lane == leader) S.wcnt[wv][cl] = __popcll(mm);
+                todo &= ~mm;
+            }
+        }
+        __syncthreads();
+        for (int t = tid; t < NS; t += NT) {
+            int h = 0;
+            for (int u = 0; u < NW; ++u) h += S.wcnt[u][t];
+            S.hist[t] = h;
         }
         __syncthreads();
         // class buckets: offsets (exclusive scan of the histogram) and each candidate's rank among the
@@ -971,9 +1038,8 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
         }
         __syncthreads();
         if (tid < m) {
-            const int c = S.cls[tid];
-            int r = 0;
-            for (int u = 0; u < tid; ++u) r += S.cls[u] == c ? 1 : 0;
+            int r = rin;
+            for (int u = 0; u < wv; ++u) r += S.wcnt[u][c];
             S.bucket[S.coff[c] + r] = tid;
             S.rank[tid] = r;
         }

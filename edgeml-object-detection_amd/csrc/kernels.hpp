@@ -48,6 +48,8 @@ struct PreParams {
     int B, H, W, Ho, Wo, Hp, Wp;
     float mean[3], stdv[3];
     float sh, sw;  // input/output scales
+    float rstd[3];  // set by the launcher: RN(1 / stdv) for the uint8 fast division (u8_fast_div)
+    int fastdiv;
 };
 
 struct DwParams {
@@ -229,6 +231,8 @@ struct StemParams {
     int H0, W0;
     float mean[3], stdv[3];
     float sh, sw;
+    float rstd[3];  // set by the launcher (u8_fast_div)
+    int fastdiv;
 };
 int ssd_stem_launch(const StemParams& p, hipStream_t s);
 int channel_mean_launch(const float* x, float* out, int B, int HW, int C, hipStream_t s);

@@ -8,6 +8,7 @@
 //   maxpool      ResNet stem max_pool2d(3,2,1); FPN LastLevelMaxPool(1,2,0) App. A.2 steps 2-3
 //   roi_align    MultiScaleRoIAlign: LevelMapper + roi_align(7x7, sr=2, aligned=False)
 //                                                                          App. A.2 step 5, row a13
+#include <cmath>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -23,9 +24,21 @@ namespace edgedet {
 // ObjectDetectionDataset.__getitem__'s `image / 255` (detect.py:55-58) on the device for a uint8
 // input: an IEEE float division (correctly rounded, as torch's CPU true_divide), so the value equals
 // the host's float image bit for bit and the rest of the transform is unchanged.
-template <typename T>
+//
+// FAST (uint8 input only): both divisions of the transform -- x / 255 and (v - mean) / std -- as a
+// multiply by the rounded reciprocal and one fma residual correction, q = RN(a r); q += RN(a - q b) r,
+// 3 instructions instead of the ~10 of a correctly rounded division.  That form is not correctly
+// rounded for every float a, but a uint8 image gives each division only 256 operands per channel, and
+// the launcher (u8_fast_div) checks all of them on the host against the IEEE division for the actual
+// mean / std, taking this path only when every one is bit-identical.
+__device__ __forceinline__ float div_fast(float a, float b, float rb) {
+    const float q = a * rb;
+    return fmaf(fmaf(-q, b, a), rb, q);
+}
+
+template <typename T, bool FAST = false>
 __device__ __forceinline__ float pre_load(const T* src, int64_t i) {
-    if constexpr (sizeof(T) == 1) return (float)src[i] / 255.f;
+    if constexpr (sizeof(T) == 1) return FAST ? div_fast((float)src[i], 255.f, 1.f / 255.f) : (float)src[i] / 255.f;
     else return src[i];
 }
 
@@ -33,9 +46,9 @@ __device__ __forceinline__ float pre_load(const T* src, int64_t i) {
 // area_pixel_compute_source_index) from image plane base xb [3][H][W]: the three channels and a zero
 // fourth.  Shared by the transform kernel and the SSD stem that folds the transform in, so both
 // produce the same bits.
-template <typename T>
+template <typename T, bool FAST = false>
 __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int W, float sh, float sw,
-                                           const float* mean, const float* stdv, int oy, int ox) {
+                                           const float* mean, const float* stdv, const float* rstd, int oy, int ox) {
     float ry = sh * ((float)oy + 0.5f) - 0.5f;
     float rx = sw * ((float)ox + 0.5f) - 0.5f;
     ry = ry < 0.f ? 0.f : ry;
@@ -49,16 +62,42 @@ __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int 
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const T* src = xb + (int64_t)c * H * W;
-        const float a00 = (pre_load(src, (int64_t)y0 * W + x0) - mean[c]) / stdv[c];
-        const float a01 = (pre_load(src, (int64_t)y0 * W + x1) - mean[c]) / stdv[c];
-        const float a10 = (pre_load(src, (int64_t)y1 * W + x0) - mean[c]) / stdv[c];
-        const float a11 = (pre_load(src, (int64_t)y1 * W + x1) - mean[c]) / stdv[c];
+        auto norm = [&](int64_t i) {
+            const float a = pre_load<T, FAST>(src, i) - mean[c];
+            return FAST ? div_fast(a, stdv[c], rstd[c]) : a / stdv[c];
+        };
+        const float a00 = norm((int64_t)y0 * W + x0);
+        const float a01 = norm((int64_t)y0 * W + x1);
+        const float a10 = norm((int64_t)y1 * W + x0);
+        const float a11 = norm((int64_t)y1 * W + x1);
         v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
     }
     return f32x4{v[0], v[1], v[2], 0.f};
 }
 
-template <typename T>
+// Host: may the uint8 transform use div_fast?  Every operand a uint8 image can give either division
+// (x = 0..255; then (x / 255 - mean_c) for each channel) is checked against the IEEE division; rstd
+// receives RN(1 / std_c).  (Host float arithmetic is IEEE single with -ffp-contract=off, fmaf exact.)
+static bool u8_fast_div(const float mean[3], const float stdv[3], float rstd[3]) {
+    const float r255 = 1.f / 255.f;
+    for (int c = 0; c < 3; ++c) rstd[c] = 1.f / stdv[c];
+    auto same = [](float a, float b) { return __builtin_memcmp(&a, &b, sizeof(float)) == 0; };
+    auto fast = [](float a, float b, float rb) {
+        const float q = a * rb;
+        return std::fma(std::fma(-q, b, a), rb, q);
+    };
+    for (int x = 0; x < 256; ++x) {
+        const float xf = (float)x, t = xf / 255.f;
+        if (!same(fast(xf, 255.f, r255), t)) return false;
+        for (int c = 0; c < 3; ++c) {
+            const float a = t - mean[c];
+            if (!same(fast(a, stdv[c], rstd[c]), a / stdv[c])) return false;
+        }
+    }
+    return true;
+}
+
+template <typename T, bool FAST>
 __global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
@@ -67,7 +106,7 @@ __global__ void preprocess_kernel(PreParams p, const T* __restrict__ x) {
     const int oy = (int)((idx / p.Wp) % p.Hp);
     const int b = (int)(idx / ((int64_t)p.Wp * p.Hp));
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
-    if (oy < p.Ho && ox < p.Wo) out = pre_pixel(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, p.mean, p.stdv, oy, ox);
+    if (oy < p.Ho && ox < p.Wo) out = pre_pixel<T, FAST>(x + (int64_t)b * 3 * p.H * p.W, p.H, p.W, p.sh, p.sw, p.mean, p.stdv, p.rstd, oy, ox);
     *reinterpret_cast<f32x4*>(p.y + idx * 4) = out;
 }
 
@@ -78,10 +117,14 @@ int preprocess_launch(const PreParams& p0, hipStream_t s) {
     p.sh = (float)p.H / (float)p.Ho;
     p.sw = (float)p.W / (float)p.Wo;
     const int64_t total = (int64_t)p.B * p.Hp * p.Wp;
-    if (p.xu8)
-        hipLaunchKernelGGL(preprocess_kernel<uint8_t>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.xu8);
-    else
-        hipLaunchKernelGGL(preprocess_kernel<float>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.x);
+    p.fastdiv = p.xu8 && u8_fast_div(p.mean, p.stdv, p.rstd);
+    if (p.xu8) {
+        void (*k)(PreParams, const uint8_t*) = p.fastdiv ? preprocess_kernel<uint8_t, true> : preprocess_kernel<uint8_t, false>;
+        hipLaunchKernelGGL(k, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.xu8);
+    } else {
+        void (*k)(PreParams, const float*) = preprocess_kernel<float, false>;
+        hipLaunchKernelGGL(k, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, s, p, p.x);
+    }
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }
@@ -182,6 +225,9 @@ __global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
 // per output drops by ~K/(1+(K-1)/PW).  Accumulation order per output is (kh, kw) as in the
 // scalar kernel.  SE variant: grid (cdiv(C/4,16), SE_PARTS, B), block = 16 quads x 16 group lanes,
 // partial sums per pixel-group split (see dwconv_se_kernel).
+#ifndef DW_PIPE
+#define DW_PIPE 0
+#endif
 template <int K, int S, int PW>
 __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restrict__ xb, int oh, int ow0, int c,
                                          f32x4 (&acc)[PW]) {
@@ -189,6 +235,39 @@ __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restr
 #pragma unroll
     for (int o = 0; o < PW; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int ih0 = oh * S - p.pad, iw0 = ow0 * S - p.pad;
+#if DW_PIPE
+    // every input row's loads issued before the first row's FMAs (clamped addresses, unconditional
+    // loads, out-of-image columns zeroed after the load; rows outside the image skipped as below, so
+    // the FMA sequence and its bits are unchanged)
+    f32x4 xin[K][IW];
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+        const int ih = min(max(ih0 + kh, 0), p.H - 1);
+        const float* row = xb + (int64_t)ih * p.W * p.C;
+#pragma unroll
+        for (int j = 0; j < IW; ++j) {
+            const int iw = iw0 + j;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(row + (int64_t)min(max(iw, 0), p.W - 1) * p.C);
+            xin[kh][j] = (unsigned)iw < (unsigned)p.W ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+        if ((unsigned)(ih0 + kh) >= (unsigned)p.H) continue;
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+            const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * K + kw) * p.C + c);
+#pragma unroll
+            for (int o = 0; o < PW; ++o) {
+                const f32x4 xv = xin[kh][o * S + kw];
+                acc[o].x = fmaf(xv.x, wv.x, acc[o].x);
+                acc[o].y = fmaf(xv.y, wv.y, acc[o].y);
+                acc[o].z = fmaf(xv.z, wv.z, acc[o].z);
+                acc[o].w = fmaf(xv.w, wv.w, acc[o].w);
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int kh = 0; kh < K; ++kh) {
         const int ih = ih0 + kh;
@@ -214,6 +293,7 @@ __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restr
             }
         }
     }
+#endif
 }
 
 template <int K, int S, int PW>
@@ -344,7 +424,7 @@ constexpr int STEM_W0 = 0, STEM_B0 = 576, STEM_WD = 592, STEM_BD = 736, STEM_W1 
 // T = float: the transform's NHWC4 output (p.x); T = float / uint8_t with FUSED: the source image
 // (p.src / p.src8, [B][3][H0][W0]) and the transform computed per input pixel of the tile (pre_pixel,
 // the same bits as the transform kernel): no transform launch and no NHWC4 round trip through HBM.
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, bool FAST = false>
 __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w) {
     __shared__ __attribute__((aligned(16))) float xs[STEM_XH * STEM_XH * 4];
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
@@ -377,7 +457,8 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             if constexpr (FUSED) {
                 const T* img = (const T*)(sizeof(T) == 1 ? (const void*)p.src8 : (const void*)p.src) +
                                (int64_t)b * 3 * p.H0 * p.W0;
-                xv[r] = in ? pre_pixel(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, ih, iw) : f32x4{0.f, 0.f, 0.f, 0.f};
+                xv[r] = in ? pre_pixel<T, FAST>(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, p.rstd, ih, iw)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
                 const float* src = xb + (in ? ((int64_t)ih * p.W + iw) * 4 : 0);  // clamped: loads stay unconditional
                 xv[r] = *reinterpret_cast<const f32x4*>(src);
@@ -481,7 +562,8 @@ int ssd_stem_launch(const StemParams& p0, hipStream_t s) {
     EDGEDET_REQUIRE(p.ld0 >= 36 && p.ld1 >= 16, "ssd_stem: weight row strides");
     const int tiles_w = cdiv(p.Wo, STEM_T);
     const dim3 grid((unsigned)(cdiv(p.Ho, STEM_T) * tiles_w), (unsigned)p.B);
-    void (*k)(StemParams, int) = p.src8 ? ssd_stem_kernel<uint8_t, true>
+    p.fastdiv = p.src8 && u8_fast_div(p.mean, p.stdv, p.rstd);
+    void (*k)(StemParams, int) = p.src8 ? (p.fastdiv ? ssd_stem_kernel<uint8_t, true, true> : ssd_stem_kernel<uint8_t, true>)
                                  : p.src ? ssd_stem_kernel<float, true> : ssd_stem_kernel<float, false>;
     hipLaunchKernelGGL(k, grid, dim3(256), 0, s, p, tiles_w);
     EDGEDET_LAUNCH_CHECK();
