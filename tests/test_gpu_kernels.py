@@ -209,7 +209,8 @@ def test_ssd_stem_folded_transform_bit_identical(H0, W0, u8):
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
-    if u8:  # the uint8 source (divided by 255 per tap, an IEEE division) equals the host's float image / 255
+    if u8:  # the uint8 source (each tap's x / 255 and (v - mean) / std by layers.hip div_fast, checked
+        # exact on every uint8 operand) equals the host's float image / 255
         srcf = (img8.float() / 255).to(DEV)
         outf = torch.full_like(outs[1], float("nan"))
         rf = rec[2:3].copy()
@@ -223,8 +224,9 @@ def test_ssd_stem_folded_transform_bit_identical(H0, W0, u8):
 
 @pytest.mark.parametrize("H0,W0", [(640, 640), (480, 640), (375, 500), (427, 640), (800, 1202)])
 def test_transform_u8_equals_float_image(H0, W0):
-    """The transform record on the decoded uint8 image (each tap divided by 255.f on the device, an
-    IEEE division) equals the transform of the host's float image / 255 (detect.py:58) bit for bit, with the FRCNN / RetinaNet
+    """The transform record on the decoded uint8 image (each tap's divisions by div_fast on the device,
+    bit-identical to the IEEE divisions on every uint8 operand: tests/test_fast_div.py) equals the
+    transform of the host's float image / 255 (detect.py:58) bit for bit, with the FRCNN / RetinaNet
     ImageNet normalisation (divisions that are not exact) and the SSD one."""
     import ctypes
     from edgeml_amd import ops
