@@ -106,14 +106,19 @@ __global__ void __launch_bounds__(256) ssd_scores_kernel(const float* __restrict
     mx = fmaxf(fmaxf(red[0][a], red[1][a]), fmaxf(red[2][a], red[3][a]));
     __syncthreads();
     float sum = 0.f;
-    for (int c = q; c < NC; c += 4) sum += expf(row[c] - mx);
+    float* rw = tile + a * ld;  // each exponential computed once: (a, c) belongs to this thread alone
+    for (int c = q; c < NC; c += 4) {
+        const float e = expf(rw[c] - mx);
+        rw[c] = e;
+        sum += e;
+    }
     red[q][a] = sum;
     __syncthreads();
     sum = ((red[0][a] + red[1][a]) + red[2][a]) + red[3][a];
     const float inv = 1.f / sum;
     if (a < na) {
         float* st = scores_t + (int64_t)b * NC * A + a0 + a;
-        for (int c = q; c < NC; c += 4) st[(int64_t)c * A] = expf(row[c] - mx) * inv;
+        for (int c = q; c < NC; c += 4) st[(int64_t)c * A] = rw[c] * inv;
         if (q == 0) {
             const int64_t idx = (int64_t)b * A + a0 + a;
             const f32x4 d = *reinterpret_cast<const f32x4*>(reg + idx * 4);
@@ -125,6 +130,7 @@ __global__ void __launch_bounds__(256) ssd_scores_kernel(const float* __restrict
 }
 
 // ================================================================ FRCNN RoIHeads: softmax + decode
+constexpr int BOX_MAXNC = 128;
 // One wave per RoI, lanes over classes.  pred [B*R][ld] with cls logits at [cls_off, +NC) and class
 // deltas at [delta_off, +4*NC) (delta_off 16-byte aligned); proposals [B][R][4];
 // -> scores [B][R][NC], boxes [B][R][NC][4].
@@ -142,13 +148,21 @@ __global__ void box_scores_kernel(const float* __restrict__ pred, int ld, int cl
     float mx = -__builtin_inff();
     for (int c = lane; c < NC; c += 64) mx = fmaxf(mx, row[c]);
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float sum = 0.f;
-    for (int c = lane; c < NC; c += 64) sum += expf(row[c] - mx);
+    float sum = 0.f, ex[BOX_MAXNC / 64];  // each exponential computed once (NC <= BOX_MAXNC)
+#pragma unroll
+    for (int u = 0; u < BOX_MAXNC / 64; ++u) {
+        const int c = lane + 64 * u;
+        ex[u] = c < NC ? expf(row[c] - mx) : 0.f;
+        if (c < NC) sum += ex[u];
+    }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
     const float inv = 1.f / sum;
     const f32x4 an = *reinterpret_cast<const f32x4*>(props + roi * 4);
-    for (int c = lane; c < NC; c += 64) {
-        scores[roi * NC + c] = expf(row[c] - mx) * inv;
+#pragma unroll
+    for (int u = 0; u < BOX_MAXNC / 64; ++u) {
+        const int c = lane + 64 * u;
+        if (c >= NC) continue;
+        scores[roi * NC + c] = ex[u] * inv;
         const f32x4 d = *reinterpret_cast<const f32x4*>(drow + 4 * c);
         f32x4 bx = decode_box(d, an, 10.f, 10.f, 5.f, 5.f);
         *reinterpret_cast<f32x4*>(boxes + (roi * NC + c) * 4) = clip_box(bx, img_h, img_w);
@@ -214,6 +228,14 @@ struct SegSmem {
     int wsum[32];
     int misc[32];
     unsigned char valid[KC];
+};
+
+template <int KC>
+struct SelSmem {  // selection-only kernels: no mask / box image
+    unsigned long long keys[KC];
+    unsigned int hist[256];
+    int wsum[32];
+    int misc[32];
 };
 
 __device__ __forceinline__ unsigned long long make_key(uint32_t k, uint32_t i) {
@@ -603,6 +625,86 @@ __device__ __forceinline__ bool iou_gt(f32x4 a, float area_a, f32x4 b, float are
 // Greedy NMS over S.box[0..m) in sorted order.  In: S.valid = candidate may be kept (invalid ones
 // neither survive nor suppress).  Out: S.valid = kept.  If `groups`, only pairs with equal
 // S.aux[] group ids interact (batched_nms).
+// The greedy scan of a segment's suppression mask (rows of NWORDS 64-bit words, word w of row i: the
+// later candidates j in [64w, 64w + 64) that i suppresses; only words w >= i / 64 are read).  In:
+// valid[j] = candidate may be kept (invalid ones neither survive nor suppress).  Out: valid = kept.
+// Run by one wave (threads 0..63 of the caller).
+template <int KC>
+__device__ __forceinline__ void nms_scan(const unsigned long long* __restrict__ mask, unsigned char* valid, int m) {
+    constexpr int NWORDS = KC / 64;
+    const int nw = (m + 63) >> 6;
+    const int lane = threadIdx.x;
+    // lane w holds word w of the suppressed set; invalid candidates start suppressed
+    unsigned long long removed = 0ull;
+    if (lane < nw) {
+        for (int jj = 0; jj < 64; ++jj) {
+            const int j = lane * 64 + jj;
+            if (j >= m || !valid[j]) removed |= 1ull << jj;
+        }
+    }
+    for (int blk = 0; blk < nw; ++blk) {
+        unsigned long long cur =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(removed >> 32), blk) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(removed & 0xffffffffu), blk);
+        const int row = blk * 64 + lane;
+        const unsigned long long diag = row < m ? mask[row * NWORDS + blk] : 0ull;
+        unsigned long long kept = 0ull;
+        unsigned long long avail = ~cur;
+        while (avail) {
+            const int l = __builtin_ctzll(avail);  // earliest candidate still alive
+            kept |= 1ull << l;
+            const unsigned long long d =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(diag >> 32), l) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(diag & 0xffffffffu), l);
+            cur |= d | (1ull << l);
+            if (l == 63) break;
+            avail = ~cur & ~((2ull << l) - 1ull);
+        }
+        if (lane > blk && lane < nw) {
+            // the kept rows' words, eight loads in flight at a time (a row taken twice ORs the same bits)
+            unsigned long long kk = kept, acc = 0ull;
+            while (kk) {
+                int ls[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    ls[u] = kk ? __builtin_ctzll(kk) : ls[0];
+                    kk &= kk - 1ull;
+                }
+                unsigned long long v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = mask[(blk * 64 + ls[u]) * NWORDS + lane];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc |= v[u];
+            }
+            removed |= acc;
+        }
+        if (row < m) valid[row] = (unsigned char)((kept >> lane) & 1ull);
+    }
+}
+
+// Word w of mask row i over the candidate boxes bx[0..m) (sorted order): bit j - 64w set when j > i
+// overlaps i beyond the threshold (same group only, if groups).
+__device__ __forceinline__ unsigned long long nms_mask_word(const f32x4* bx, const int* grp, int m, int i, int w,
+                                                            const IouThr& thr) {
+    unsigned long long bits = 0ull;
+    const f32x4 bi = bx[i];
+    const float ai = (bi.z - bi.x) * (bi.w - bi.y);
+    const int gi = grp ? grp[i] : 0;
+    const int j0 = w * 64;
+    const int jend = min(m, j0 + 64);
+#pragma unroll NMS_UNROLL
+    for (int j = max(j0, i + 1); j < jend; ++j) {
+        if (grp && grp[j] != gi) continue;
+        const f32x4 bj = bx[j];
+        const float aj = (bj.z - bj.x) * (bj.w - bj.y);
+        if (iou_gt(bi, ai, bj, aj, thr)) bits |= 1ull << (j - j0);
+    }
+    return bits;
+}
+
+// Greedy NMS over S.box[0..m) in sorted order.  In: S.valid = candidate may be kept (invalid ones
+// neither survive nor suppress).  Out: S.valid = kept.  If `groups`, only pairs with equal
+// S.aux[] group ids interact (batched_nms).
 template <int NT, int KC>
 __device__ void nms_block(SegSmem<KC>& S, int m, const IouThr& thr, bool groups) {
     constexpr int NWORDS = KC / 64;
@@ -611,72 +713,18 @@ __device__ void nms_block(SegSmem<KC>& S, int m, const IouThr& thr, bool groups)
     // while their own rows are consecutive (w-fastest put 16 lanes on one bank, 1 KiB apart)
     for (int t = threadIdx.x; t < m * nw; t += NT) {
         const int w = t / m, i = t - w * m;
-        unsigned long long bits = 0ull;
-        if (w >= (i >> 6)) {
-            const f32x4 bi = S.box[i];
-            const float ai = (bi.z - bi.x) * (bi.w - bi.y);
-            const int gi = groups ? S.aux[i] : 0;
-            const int j0 = w * 64;
-            const int jend = min(m, j0 + 64);
-#pragma unroll NMS_UNROLL
-            for (int j = max(j0, i + 1); j < jend; ++j) {
-                if (groups && S.aux[j] != gi) continue;
-                const f32x4 bj = S.box[j];
-                const float aj = (bj.z - bj.x) * (bj.w - bj.y);
-                if (iou_gt(bi, ai, bj, aj, thr)) bits |= 1ull << (j - j0);
-            }
-        }
-        S.mask[i * NWORDS + w] = bits;
+        S.mask[i * NWORDS + w] = w >= (i >> 6) ? nms_mask_word(S.box, groups ? S.aux : nullptr, m, i, w, thr) : 0ull;
     }
     __syncthreads();
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        // lane w holds word w of the suppressed set; invalid candidates start suppressed
-        unsigned long long removed = 0ull;
-        if (lane < nw) {
-            for (int jj = 0; jj < 64; ++jj) {
-                const int j = lane * 64 + jj;
-                if (j >= m || !S.valid[j]) removed |= 1ull << jj;
-            }
-        }
-        for (int blk = 0; blk < nw; ++blk) {
-            unsigned long long cur =
-                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(removed >> 32), blk) << 32) |
-                (uint32_t)__builtin_amdgcn_readlane((int)(removed & 0xffffffffu), blk);
-            const int row = blk * 64 + lane;
-            const unsigned long long diag = row < m ? S.mask[row * NWORDS + blk] : 0ull;
-            unsigned long long kept = 0ull;
-            unsigned long long avail = ~cur;
-            while (avail) {
-                const int l = __builtin_ctzll(avail);  // earliest candidate still alive
-                kept |= 1ull << l;
-                const unsigned long long d =
-                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(diag >> 32), l) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)(diag & 0xffffffffu), l);
-                cur |= d | (1ull << l);
-                if (l == 63) break;
-                avail = ~cur & ~((2ull << l) - 1ull);
-            }
-            if (lane > blk && lane < nw) {
-                unsigned long long kk = kept, acc = 0ull;
-                while (kk) {
-                    const int l = __builtin_ctzll(kk);
-                    kk &= kk - 1ull;
-                    acc |= S.mask[(blk * 64 + l) * NWORDS + lane];
-                }
-                removed |= acc;
-            }
-            if (row < m) S.valid[row] = (unsigned char)((kept >> lane) & 1ull);
-        }
-    }
+    if (threadIdx.x < 64) nms_scan<KC>(S.mask, S.valid, m);
     __syncthreads();
 }
 
 // Per-segment kept lists (records) consumed by merge_topk.
 
 // Write the kept candidates of a segment in sorted order.  rec(t, slot_offset) writes one record.
-template <int NT, int KC, typename W>
-__device__ void write_kept(SegSmem<KC>& S, int m, int seg, const SegOut& out, W rec) {
+template <int NT, int KC, typename SM, typename W>
+__device__ void write_kept(SM& S, int m, int seg, const SegOut& out, W rec) {
     int written = 0;
     for (int base = 0; base < m; base += NT) {
         const int t = base + threadIdx.x;
@@ -1223,7 +1271,7 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
 template <int NT, int KC>
 __global__ void __launch_bounds__(NT) rpn_chunk_select_kernel(RpnParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    SegSmem<KC>& S = *reinterpret_cast<SegSmem<KC>*>(smem_raw);
+    SelSmem<KC>& S = *reinterpret_cast<SelSmem<KC>*>(smem_raw);
     const int c = blockIdx.x, l = blockIdx.y, b = blockIdx.z;
     const RpnLevel L = P.lv[l];
     const int64_t slot = ((int64_t)(b * P.nlevels + l) * P.nchunk + c);
@@ -1308,6 +1356,160 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
     write_kept<NT, KC>(S, m, b * P.nlevels + l, out, [&](int t, int64_t o) {
         const float logit = key_float((uint32_t)(S.keys[t] >> 32));
         out.box[o] = S.box[t];
+        out.score[o] = 1.f / (1.f + expf(-logit));
+        out.tb[o] = ((uint32_t)l << 16) | (uint32_t)t;  // concatenation order: (level, rank)
+        out.label[o] = l;
+    });
+}
+
+// ---------------------------------------------------------------- RPN level NMS, split form
+// The level kernel above runs the whole segment (select, sort, decode, the m x m IoU mask, the greedy
+// scan) in one workgroup per (level, image): 40 workgroups for FRCNN b = 8, each holding a CU for the
+// whole O(m^2) mask.  The split form runs the same arithmetic as three launches -- the selection per
+// segment (rpn_level_select_kernel, small LDS), the mask rows in 64-row blocks over KC / 64 x segments
+// workgroups (rpn_mask_kernel), the scan and the kept records per segment (rpn_level_scan_kernel, the
+// mask staged in LDS) -- with the intermediates in one scratch buffer (RpnSplit).
+struct RpnSplit {
+    unsigned long long* mask;  // [seg][KC][KC / 64]
+    f32x4* box;                // [seg][KC]
+    unsigned long long* key;   // [seg][KC]
+    unsigned char* valid;      // [seg][KC]
+    int* m;                    // [seg]
+};
+constexpr int RPN_KC = 1024;
+static inline int64_t rs_align(int64_t x) { return (x + 255) / 256 * 256; }
+int64_t rpn_split_bytes(int64_t nseg) {
+    return rs_align(nseg * RPN_KC * (RPN_KC / 64) * 8) + rs_align(nseg * RPN_KC * 16) + rs_align(nseg * RPN_KC * 8) +
+           rs_align(nseg * RPN_KC) + rs_align(nseg * 4);
+}
+static RpnSplit rpn_split(void* base, int64_t nseg) {
+    unsigned char* q = (unsigned char*)base;
+    RpnSplit X;
+    X.mask = (unsigned long long*)q;
+    q += rs_align(nseg * RPN_KC * (RPN_KC / 64) * 8);
+    X.box = (f32x4*)q;
+    q += rs_align(nseg * RPN_KC * 16);
+    X.key = (unsigned long long*)q;
+    q += rs_align(nseg * RPN_KC * 8);
+    X.valid = q;
+    q += rs_align(nseg * RPN_KC);
+    X.m = (int*)q;
+    return X;
+}
+
+template <int NT, int KC>
+__global__ void __launch_bounds__(NT) rpn_level_select_kernel(RpnParams P, RpnSplit X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    SelSmem<KC>& S = *reinterpret_cast<SelSmem<KC>*>(smem_raw);
+    const int l = blockIdx.x, b = blockIdx.y;
+    const int seg = b * P.nlevels + l;
+    const RpnLevel L = P.lv[l];
+    const float* ob = L.obj + (int64_t)b * L.n;
+    const f32x4* db = reinterpret_cast<const f32x4*>(L.deltas) + (int64_t)b * L.n;
+    const bool chunked = P.ckey != nullptr;
+    const int64_t cbase = (int64_t)seg * P.nchunk;
+    const uint32_t* ck = chunked ? P.ckey + cbase * KC : nullptr;
+    const int* ci = chunked ? P.cidx + cbase * KC : nullptr;
+    const int* cc = chunked ? P.ccount + cbase : nullptr;
+    const int n = chunked ? (L.n + P.chunk - 1) / P.chunk * KC : L.n;
+    auto fkey = [&](int i, uint32_t& k) -> bool {
+        if (!chunked) {
+            k = float_key(ob[i]);
+            return true;
+        }
+        const int ch = i / KC, r = i - ch * KC;
+        k = ck[i];
+        return r < cc[ch];
+    };
+    auto level_index = [&](int i) { return chunked ? ci[i] : i; };
+    const uint32_t T = radix_select<NT>(n, P.topk, fkey, S.hist, S.misc);
+    const bool take_all = S.misc[1] <= P.topk;
+    const int m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    bitonic_desc<NT>(S.keys, nullptr, m);
+    for (int t = threadIdx.x; t < m; t += NT) {
+        const int i = level_index(key_index(S.keys[t]));
+        const f32x4 d = db[i];
+        const f32x4 an = *reinterpret_cast<const f32x4*>(L.anchors + (int64_t)i * 4);
+        const f32x4 bx = clip_box(decode_box(d, an, 1.f, 1.f, 1.f, 1.f), P.img_h, P.img_w);
+        const float logit = key_float((uint32_t)(S.keys[t] >> 32));
+        const float score = 1.f / (1.f + expf(-logit));
+        const int64_t o = (int64_t)seg * KC + t;
+        X.box[o] = bx;
+        X.key[o] = S.keys[t];
+        X.valid[o] = ((bx.z - bx.x) >= P.min_size && (bx.w - bx.y) >= P.min_size && score >= P.score_thresh) ? 1 : 0;
+    }
+    if (threadIdx.x == 0) X.m[seg] = m;
+}
+
+// grid (KC / 64 row blocks, levels, images): mask rows [64 rb, 64 rb + 64) of the segment, words
+// w >= rb (the only ones the scan reads), the segment's boxes from 64 rb on staged in LDS
+template <int KC>
+__global__ void __launch_bounds__(256) rpn_mask_kernel(RpnSplit X, int nlevels, IouThr thr) {
+    constexpr int NWORDS = KC / 64;
+    __shared__ f32x4 sb[KC];
+    const int rb = blockIdx.x, seg = blockIdx.z * nlevels + blockIdx.y;
+    const int m = X.m[seg];
+    const int nw = (m + 63) >> 6;
+    if (rb >= nw) return;
+    const f32x4* gb = X.box + (int64_t)seg * KC;
+    {  // every load of the thread issued before any store (clamped indices)
+        f32x4 v[KC / 256];
+#pragma unroll
+        for (int u = 0; u < KC / 256; ++u) v[u] = gb[min(64 * rb + (int)threadIdx.x + 256 * u, m - 1)];
+#pragma unroll
+        for (int u = 0; u < KC / 256; ++u) {
+            const int t = 64 * rb + (int)threadIdx.x + 256 * u;
+            if (t < m) sb[t] = v[u];
+        }
+    }
+    __syncthreads();
+    const int i0 = 64 * rb, ni = min(64, m - i0), ntask = ni * (nw - rb);
+    unsigned long long* gm = X.mask + (int64_t)seg * KC * NWORDS;
+    for (int t = threadIdx.x; t < ntask; t += 256) {  // row fastest across lanes, as nms_block
+        const int w = rb + t / ni, i = i0 + t % ni;
+        gm[i * NWORDS + w] = nms_mask_word(sb, nullptr, m, i, w, thr);
+    }
+}
+
+template <int KC>
+struct ScanSmem {
+    unsigned long long mask[KC * (KC / 64)];
+    unsigned char valid[KC];
+    int wsum[32];
+};
+
+template <int NT, int KC>
+__global__ void __launch_bounds__(NT) rpn_level_scan_kernel(RpnParams P, RpnSplit X, SegOut out) {
+    constexpr int NWORDS = KC / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    ScanSmem<KC>& S = *reinterpret_cast<ScanSmem<KC>*>(smem_raw);
+    const int l = blockIdx.x, b = blockIdx.y;
+    const int seg = b * P.nlevels + l;
+    const int m = X.m[seg];
+    const unsigned long long* gm = X.mask + (int64_t)seg * KC * NWORDS;
+    // rows i < m as 16-byte pairs of words, eight loads of each thread in flight before its stores (the
+    // words below a row's own block were never written and are never read)
+    {
+        const int n2 = m * NWORDS / 2;
+        const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(gm);
+        ulonglong2* s2 = reinterpret_cast<ulonglong2*>(S.mask);
+        for (int base = threadIdx.x; base < n2; base += NT * 8) {
+            ulonglong2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = g2[min(base + NT * u, n2 - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (base + NT * u < n2) s2[base + NT * u] = v[u];
+        }
+    }
+    for (int t = threadIdx.x; t < m; t += NT) S.valid[t] = X.valid[(int64_t)seg * KC + t];
+    __syncthreads();
+    if (threadIdx.x < 64) nms_scan<KC>(S.mask, S.valid, m);
+    __syncthreads();
+    write_kept<NT, KC>(S, m, seg, out, [&](int t, int64_t o) {
+        const unsigned long long key = X.key[(int64_t)seg * KC + t];
+        const float logit = key_float((uint32_t)(key >> 32));
+        out.box[o] = X.box[(int64_t)seg * KC + t];
         out.score[o] = 1.f / (1.f + expf(-logit));
         out.tb[o] = ((uint32_t)l << 16) | (uint32_t)t;  // concatenation order: (level, rank)
         out.label[o] = l;
@@ -1669,6 +1871,7 @@ int box_scores_launch(const float* pred, int ld, int cls_off, int delta_off, con
                       float* scores, float* boxes, int B, int R, int NC, float img_h, float img_w, hipStream_t s) {
     EDGEDET_REQUIRE(pred && props && counts && scores && boxes, "box_scores: null pointer");
     EDGEDET_REQUIRE(ld >= 5 * NC && ld % 4 == 0 && delta_off % 4 == 0, "box_scores: bad predictor layout");
+    EDGEDET_REQUIRE(NC >= 1 && NC <= BOX_MAXNC, "box_scores: 1..128 classes");
     const int64_t total = (int64_t)B * R;
     hipLaunchKernelGGL(box_scores_kernel, dim3((unsigned)cdiv(total, 4)), dim3(256), 0, s, pred, ld, cls_off,
                        delta_off, props, counts, scores, boxes, B, R, NC, img_h, img_w);
@@ -1734,9 +1937,24 @@ int rpn_level_nms_launch(const RpnParams& P, SegOut out, hipStream_t s) {
         for (int l = 0; l < P.nlevels; ++l)
             EDGEDET_REQUIRE((P.lv[l].n + P.chunk - 1) / P.chunk <= P.nchunk, "rpn: a level exceeds nchunk chunks");
         auto k1 = rpn_chunk_select_kernel<NT, KC>;
-        if (set_lds(k1, seg_smem<KC>())) return -2;
-        hipLaunchKernelGGL(k1, dim3(P.nchunk, P.nlevels, P.B), dim3(NT), seg_smem<KC>(), s, P);
+        if (set_lds(k1, sizeof(SelSmem<KC>))) return -2;
+        hipLaunchKernelGGL(k1, dim3(P.nchunk, P.nlevels, P.B), dim3(NT), sizeof(SelSmem<KC>), s, P);
         EDGEDET_LAUNCH_CHECK();
+    }
+    if (P.split) {
+        static_assert(KC == RPN_KC, "split scratch layout");
+        const RpnSplit X = rpn_split(P.split, (int64_t)P.B * P.nlevels);
+        auto k1 = rpn_level_select_kernel<NT, KC>;
+        if (set_lds(k1, sizeof(SelSmem<KC>))) return -2;
+        hipLaunchKernelGGL(k1, dim3(P.nlevels, P.B), dim3(NT), sizeof(SelSmem<KC>), s, P, X);
+        EDGEDET_LAUNCH_CHECK();
+        hipLaunchKernelGGL(rpn_mask_kernel<KC>, dim3(KC / 64, P.nlevels, P.B), dim3(256), 0, s, X, P.nlevels, P.iou);
+        EDGEDET_LAUNCH_CHECK();
+        auto k3 = rpn_level_scan_kernel<NT, KC>;
+        if (set_lds(k3, sizeof(ScanSmem<KC>))) return -2;
+        hipLaunchKernelGGL(k3, dim3(P.nlevels, P.B), dim3(NT), sizeof(ScanSmem<KC>), s, P, X, out);
+        EDGEDET_LAUNCH_CHECK();
+        return 0;
     }
     auto k = rpn_level_nms_kernel<NT, KC>;
     if (set_lds(k, seg_smem<KC>())) return -2;

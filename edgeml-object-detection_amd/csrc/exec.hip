@@ -36,7 +36,8 @@
 //   RPN_LEVEL_NMS  p0..4 objectness [B][n] per level; p5..9 anchors per level; p10..14 records;
 //                  p15..19 deltas [B][n][4] per level; i0..5 B,nlevels,(unused),A,topk,kmax; i6..10 n per level;
 //                  f0..3 img_h,img_w,min_size,score_thresh; d0 iou; chunked top-k (optional): p20 ckey,
-//                  p21 cidx [B,levels,nchunk,1024], p22 ccount [B,levels,nchunk]; i16 chunk; i17 nchunk
+//                  p21 cidx [B,levels,nchunk,1024], p22 ccount [B,levels,nchunk]; i16 chunk; i17 nchunk;
+//                  split NMS scratch (optional) p23 [rpn_split_bytes(B * levels)]
 //   ROI_ALIGN      p0..3 feats; p4 rois; p5 counts; p6 out; i0..10 mode,R,RMAX,B,C,PH,PW,sr,nlevels,
 //                  k_min,k_max; i11..14 H; i15..18 W; f0..3 scales
 //   BOX_SCORES     p0 pred; p1 props; p2 counts; p3 scores; p4 boxes; i0..5 ld,B,R,NC,cls_off,delta_off;
@@ -313,6 +314,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.ccount = P<int>(o, 22);
             p.chunk = (int)I[16];
             p.nchunk = (int)I[17];
+            p.split = P<void>(o, 23);
             return rpn_level_nms_launch(p, seg_out(o, 10, (int)I[5]), s);
         }
         case EDGEDET_OP_ROI_ALIGN: {

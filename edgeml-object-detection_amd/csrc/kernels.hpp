@@ -141,7 +141,11 @@ struct RpnParams {
     int* cidx;
     int* ccount;
     int chunk, nchunk;
+    // split NMS (optional, split != null): selection, the IoU mask over many workgroups and the greedy
+    // scan as three launches, the intermediates in this scratch (rpn_split_bytes(B * nlevels))
+    void* split;
 };
+int64_t rpn_split_bytes(int64_t nseg);
 
 struct MergeParams {
     const f32x4* box;

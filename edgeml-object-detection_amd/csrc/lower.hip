@@ -1353,6 +1353,10 @@ class FasterRCNN : public ResNetFPN {
             o.p[22] = P.ref(P.buf({B, L, nch}, I32, "rpn.chunk.count"));
             o.i[16] = chunk;
             o.i[17] = nch;
+            // split NMS (selection / IoU mask over many workgroups / scan): EDGEDET_RPN_SPLIT=0 keeps one
+            // workgroup per (level, image) for the whole segment
+            if (env_int("EDGEDET_RPN_SPLIT", 1))
+                o.p[23] = P.ref(P.buf({rpn_split_bytes((int64_t)B * L)}, 1, "rpn.nms.split"));
             P.add(o);
         }
         const int R = RPN_POST;

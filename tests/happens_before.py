@@ -41,7 +41,7 @@ ROLES = {
     ops.SSD_CLASS_NMS: {0: R, 1: R, 2: W, 3: W, 4: W, 5: W, 6: W},
     ops.MERGE_TOPK: {0: R, 1: R, 2: R, 3: R, 4: R, 5: R, 6: W, 7: W, 8: W, 9: W},
     ops.RPN_LEVEL_NMS: dict([(j, R) for j in range(10)] + [(j, R) for j in range(15, 20)] +
-                            [(j, W) for j in range(10, 15)] + [(j, RW) for j in (20, 21, 22)]),
+                            [(j, W) for j in range(10, 15)] + [(j, RW) for j in (20, 21, 22, 23)]),
     ops.ROI_ALIGN: {0: R, 1: R, 2: R, 3: R, 4: R, 5: R, 6: W},
     ops.BOX_SCORES: {0: R, 1: R, 2: R, 3: W, 4: W},
     ops.BOX_CLASS_NMS: {0: R, 1: R, 2: R, 3: W, 4: W, 5: W, 6: W, 7: W},
