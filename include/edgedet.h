@@ -60,7 +60,8 @@ enum {
     EDGEDET_OP_SSD_CLASS_NMS = 9, /* per (image, class): score>t, top-k, NMS                          */
     EDGEDET_OP_MERGE_TOPK = 10,   /* per image: merge kept lists, sort by score, keep[:N], rescale    */
     EDGEDET_OP_RPN_LEVEL_NMS = 11,/* per (image, FPN level): top-k logits, decode, clip, small, NMS
-                                   * (with p20..p22 a chunked top-k: per-chunk lists first)          */
+                                   * (with p20..p22 a chunked top-k: per-chunk lists first; with p23
+                                   * the NMS split into selection / IoU mask / scan launches)        */
     EDGEDET_OP_ROI_ALIGN = 12,    /* MultiScaleRoIAlign (LevelMapper + roi_align 7x7, sr=2)          */
     EDGEDET_OP_BOX_SCORES = 13,   /* RoIHeads softmax + class-specific decode + clip                 */
     EDGEDET_OP_BOX_CLASS_NMS = 14,/* per (image, class): score>t, remove_small, NMS                   */
