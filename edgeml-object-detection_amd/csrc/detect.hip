@@ -236,6 +236,8 @@ struct SelSmem {  // selection-only kernels: no mask / box image
     unsigned int hist[256];
     int wsum[32];
     int misc[32];
+    int red[64];
+    unsigned long long run[KC];  // rank_sort_desc
 };
 
 __device__ __forceinline__ unsigned long long make_key(uint32_t k, uint32_t i) {
@@ -552,47 +554,57 @@ __device__ void bitonic_desc(unsigned long long* keys, int* payload, int m) {
     }
 }
 
-// Sort of keys[0..m) descending for m <= NT, one key per thread, two barriers: each wave ranks its 64
-// keys among themselves (a readlane walk: keys greater, equal keys at lower lanes first) and writes its
-// run sorted into run[]; a key's final position is its rank in its own run plus, for every other run, the
-// number of that run's keys ahead of it (binary search; equal keys: the earlier run first).  Keys past m
-// are zeros and sort last.  Replaces the 45 barrier stages of a 512-key bitonic sort.
-template <int NT>
+// Sort of keys[0..m) descending for m <= U * NT (U keys per thread: key tid + NT * u), two barriers:
+// each 64-key run (the keys of one wave's slot u) is ranked within itself (a readlane walk: keys
+// greater, equal keys at lower lanes first) and written sorted into run[]; a key's final position is
+// its rank in its own run plus, for every other run, the number of that run's keys ahead of it
+// (binary search; equal keys: the earlier run first).  Keys past m are zeros and sort last.
+// Replaces the 45 (512 keys) / 55 (1,024) barrier stages of a bitonic sort.
+template <int NT, int U = 1>
 __device__ void rank_sort_desc(unsigned long long* keys, unsigned long long* run, int m) {
-    constexpr int NW = NT / 64;
+    constexpr int NR = U * NT / 64;  // runs
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const unsigned long long k = tid < m ? keys[tid] : 0ull;
-    int r = 0;
-    if (64 * w < m) {  // wave-uniform: waves wholly past m write zeros below
-        const uint32_t klo = (uint32_t)k, khi = (uint32_t)(k >> 32);
+    unsigned long long k[U];
+    int r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = tid + NT * u, rid = e >> 6;
+        k[u] = e < m ? keys[e] : 0ull;
+        r[u] = lane;
+        if (64 * rid < m) {  // wave-uniform: runs wholly past m hold zeros in lane order
+            const uint32_t klo = (uint32_t)k[u], khi = (uint32_t)(k[u] >> 32);
+            int c = 0;
 #pragma unroll 16
-        for (int j = 0; j < 64; ++j) {
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)khi, j);
-            const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
-            r += (kj > k || (kj == k && j < lane)) ? 1 : 0;
-        }
-    } else {
-        r = lane;
-    }
-    run[64 * w + r] = k;
-    __syncthreads();
-    int pos = r;
-#pragma unroll
-    for (int v = 0; v < NW; ++v) {
-        if (v == w || 64 * v >= m) continue;  // a run wholly past m holds only zeros, after every key
-        const unsigned long long* rv = run + 64 * v;
-        int lo = 0;
-#pragma unroll
-        for (int st = 64; st >= 1; st >>= 1) {
-            if (lo + st <= 64) {
-                const unsigned long long e = rv[lo + st - 1];
-                if (e > k || (e == k && v < w)) lo += st;
+            for (int j = 0; j < 64; ++j) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)khi, j);
+                const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
+                c += (kj > k[u] || (kj == k[u] && j < lane)) ? 1 : 0;
             }
+            r[u] = c;
         }
-        pos += lo;
+        run[64 * rid + r[u]] = k[u];
     }
-    if (tid < m) keys[pos] = k;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = tid + NT * u, rid = e >> 6;
+        int pos = r[u];
+        for (int v = 0; v < NR; ++v) {
+            if (v == rid || 64 * v >= m) continue;  // a run wholly past m holds only zeros, after every key
+            const unsigned long long* rv = run + 64 * v;
+            int lo = 0;
+#pragma unroll
+            for (int st = 64; st >= 1; st >>= 1) {
+                if (lo + st <= 64) {
+                    const unsigned long long x = rv[lo + st - 1];
+                    if (x > k[u] || (x == k[u] && v < rid)) lo += st;
+                }
+            }
+            pos += lo;
+        }
+        if (e < m) keys[pos] = k[u];
+    }
     __syncthreads();
 }
 
@@ -1376,7 +1388,7 @@ struct RpnSplit {
     unsigned char* valid;      // [seg][KC]
     int* m;                    // [seg]
 };
-constexpr int RPN_KC = 1024;
+constexpr int RPN_KC = 1024, RPN_PER = 32;  // register path: chunk unions of <= 16 chunks
 static inline int64_t rs_align(int64_t x) { return (x + 255) / 256 * 256; }
 int64_t rpn_split_bytes(int64_t nseg) {
     return rs_align(nseg * RPN_KC * (RPN_KC / 64) * 8) + rs_align(nseg * RPN_KC * 16) + rs_align(nseg * RPN_KC * 8) +
@@ -1422,10 +1434,27 @@ __global__ void __launch_bounds__(NT) rpn_level_select_kernel(RpnParams P, RpnSp
         return r < cc[ch];
     };
     auto level_index = [&](int i) { return chunked ? ci[i] : i; };
-    const uint32_t T = radix_select<NT>(n, P.topk, fkey, S.hist, S.misc);
-    const bool take_all = S.misc[1] <= P.topk;
-    const int m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
-    bitonic_desc<NT>(S.keys, nullptr, m);
+    int m;
+    if (chunked && n <= NT * RPN_PER) {
+        // the chunk union held in registers (element i = threadIdx.x + NT * j, 0 = not a candidate):
+        // the bisection top-k of select_topk_regs takes the same set as the radix select + compaction
+        // below -- the top-k by (key desc, list position asc) -- with one barrier per probe instead of
+        // four streaming passes with LDS histograms
+        uint32_t kr[RPN_PER];
+#pragma unroll
+        for (int j = 0; j < RPN_PER; ++j) {
+            const int i = (int)threadIdx.x + NT * j, ic = i < n ? i : n - 1;
+            const int ch = ic / KC;
+            const uint32_t k = ck[ic];
+            kr[j] = (i < n && ic - ch * KC < cc[ch]) ? k : 0u;
+        }
+        m = select_topk_regs<NT, RPN_PER>(kr, P.topk, KC, S.keys, S.wsum, S.red);
+    } else {
+        const uint32_t T = radix_select<NT>(n, P.topk, fkey, S.hist, S.misc);
+        const bool take_all = S.misc[1] <= P.topk;
+        m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
+    }
+    rank_sort_desc<NT, KC / NT>(S.keys, S.run, m);
     for (int t = threadIdx.x; t < m; t += NT) {
         const int i = level_index(key_index(S.keys[t]));
         const f32x4 d = db[i];

@@ -9,7 +9,10 @@
 * the chunked RPN top-k (RPN_LEVEL_NMS with the p20..p22 chunk scratch, csrc/detect.hip
   rpn_chunk_select_kernel) must equal the single-pass level selection bit for bit, also when exact
   ties cross the 8,192-anchor chunk and the 4,096-key compaction batch boundaries, and on a level with
-  fewer anchors than the top-k (P6: 507 < 1,000).
+  fewer anchors than the top-k (P6: 507 < 1,000); the chunk union's selection from registers (the
+  default when the union fits 32 keys per thread) against the radix selection of the single pass;
+* the split NMS (p23 scratch: selection / IoU mask over many workgroups / scan) equal to the one-
+  workgroup-per-segment kernel, chunked or not.
 """
 import ctypes
 
@@ -79,7 +82,7 @@ def test_group_launch_equals_members_one_by_one(which):
 
 
 @pytest.mark.parametrize("pattern", ["quantized", "all_equal", "continuous", "two_values"])
-def test_rpn_chunked_topk_equals_single_pass(pattern):
+def test_rpn_chunked_split_equal_single_pass(pattern):
     B = 2
     m = models.FasterRCNNFPNv2(synthetic.synthetic_state_dict("faster_rcnn", 91), 91).to("cuda")
     plan = m.plan(B, 640, 640)
@@ -106,16 +109,21 @@ def test_rpn_chunked_topk_equals_single_pass(pattern):
         d.copy_((torch.randn(B * n * 4, generator=g) * 0.2).cuda())
     sizes = [B * L * KM * 16, B * L * KM * 4, B * L * KM * 4, B * L * KM * 4, B * L * 4]
     outs = [_region(plan, rec["p"][0, 10 + j], sizes[j]) for j in range(5)]
+    assert rec["p"][0, 23], "the lowering's record carries the split-NMS scratch"
     got = []
-    for chunked in (True, False):
+    variants = [(True, True), (True, False), (False, True), (False, False)]  # (chunked, split)
+    for chunked, split in variants:
         r = rec.copy()
         if not chunked:
             r["p"][0, 20:23] = 0
+        if not split:
+            r["p"][0, 23] = 0
         for o in outs:
             o.fill_(0xFF)
         _run(r)
         got.append([o.clone() for o in outs])
     cnt = got[0][4].view(torch.int32)
     assert (cnt > 0).all(), cnt
-    for j, (a, b) in enumerate(zip(*got)):
-        assert torch.equal(a, b), (pattern, ["box", "score", "tb", "level", "count"][j])
+    for v in range(1, len(variants)):
+        for j, (a, b) in enumerate(zip(got[0], got[v])):
+            assert torch.equal(a, b), (pattern, variants[v], ["box", "score", "tb", "level", "count"][j])
