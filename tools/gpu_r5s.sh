@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-5 session s: where the table stem's output differs under concurrency (count, size, images, tiles)
+cd "$GRAFT_REPO_ROOT" || exit 9
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
+: > gpurun_out/r5s_steps.log
+D=$PWD/edgeml-object-detection_amd
+st() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/r5s_$name.log 2>&1; local rc=$?; echo "$name rc=$rc" >> gpurun_out/r5s_steps.log; if grep -q "Memory access fault\|HSA_STATUS_ERROR" gpurun_out/r5s_$name.log; then exit 7; fi; [ $rc -gt 1 ] && exit $rc; return 0; }
+st dbg_detail 300 env EDGEDET_LIB=$D/libedgedet_stemdbg.so python -u tools/race_bisect.py --kind ssd --B 32 --H 640 --W 640 --trials 8 --stem-debug --detail backbone.features.0.1
+st dbg_detail_n1 300 env EDGEDET_LIB=$D/libedgedet_stemdbg.so python -u tools/race_bisect.py --kind ssd --B 32 --H 640 --W 640 --trials 6 --n 1 --detail backbone.features.0.1
+exit 0

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--trials", type=int, default=8)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--n", type=int, default=2, help="instances in flight at once")
+    ap.add_argument("--detail", default="", help="buffer name prefix to describe when it differs (count, max |diff|, where)")
+    ap.add_argument("--stem-debug", action="store_true",
+                    help="a -DSTEM_TABLE_DEBUG build (EDGEDET_LIB): print its table-stem LDS check counters per trial")
     a = ap.parse_args()
     from edgeml_amd import models, synthetic, ops
     if a.kind == "ssd":
@@ -50,6 +53,13 @@ def main():
     go(0)
     torch.cuda.synchronize()
     ref = {b.name: b.tensor().clone() for b in bufs}
+    ref_host = {b.name: ref[b.name].cpu() for b in bufs}  # to tell a changed reference copy from a changed buffer
+    if a.stem_debug:
+        import ctypes
+        c = (ctypes.c_uint * 4)()
+        ops.check(ops.lib().edgedet_stem_debug_read(c, 1))
+        print(f"solo (capture + reference runs): stem LDS checks: table changed {c[0]}, weights changed {c[1]}, "
+              f"non-finite outputs {c[2]}", flush=True)
     for t in range(a.trials):
         for k in range(a.n):
             plans[k].input.tensor().copy_(imgs[k])
@@ -61,7 +71,37 @@ def main():
                 plans[k].replay(streams[k])
         torch.cuda.synchronize()
         bad = [b.name for b in bufs if not torch.equal(b.tensor(), ref[b.name])]
-        print(f"trial {t}: {len(bad)} of {len(bufs)} buffers differ; first: {bad[:6]}", flush=True)
+        extra = ""
+        if a.stem_debug:
+            import ctypes
+            c = (ctypes.c_uint * 4)()
+            ops.check(ops.lib().edgedet_stem_debug_read(c, 1))
+            extra = f"; stem LDS checks: table changed {c[0]}, weights changed {c[1]}, non-finite outputs {c[2]}"
+        print(f"trial {t}: {len(bad)} of {len(bufs)} buffers differ; first: {bad[:6]}{extra}", flush=True)
+        moved = [n for n in ref if not torch.equal(ref[n].cpu(), ref_host[n])]
+        if moved:
+            print(f"  the device reference copies of {len(moved)} buffers changed since they were taken "
+                  f"(writes into memory outside the plans): {moved[:6]}", flush=True)
+        if "images" in bad:
+            x, y = plans[0].input.tensor(), ref["images"]
+            d = (x != y).flatten().nonzero().flatten()
+            per_img = (x != y).flatten(1).sum(1).tolist() if x.dim() > 1 else []
+            print(f"  images: {d.numel()} bytes differ, flat offsets {int(d.min())}..{int(d.max())}, per image "
+                  f"{[(i, n) for i, n in enumerate(per_img) if n]}", flush=True)
+        if a.detail:
+            for b in bufs:
+                if b.name.startswith(a.detail) and b.name in bad:
+                    x, y = b.tensor(), ref[b.name]
+                    if x.dtype != torch.float32 or x.dim() != 4:
+                        continue
+                    d = (x != y)
+                    Bn, Hh, Ww, Cc = x.shape
+                    pix = d.any(-1)  # [B, H, W]
+                    imgs = pix.flatten(1).any(1).nonzero().flatten().tolist()
+                    tiles = sorted({(int(i), int(h) // 16, int(w) // 16) for i, h, w in pix.nonzero().tolist()})
+                    print(f"  {b.name}: {int(d.sum())} of {d.numel()} elements differ, max |diff| "
+                          f"{float((x - y).abs().max()):.3e}, images {imgs}, {len(tiles)} differing 16x16 output "
+                          f"tiles of {Bn * ((Hh + 15) // 16) * ((Ww + 15) // 16)}; first tiles {tiles[:8]}", flush=True)
 
 
 if __name__ == "__main__":
