@@ -106,10 +106,17 @@ __device__ __forceinline__ f32x4 pre_pixel_lut(const uint8_t* __restrict__ xb, i
     for (int c = 0; c < 3; ++c) {
         const uint8_t* src = xb + (int64_t)c * H * W;
         const float* t = lut + 256 * c;
+#if STEM_TABLE_DEBUG > 1  // every byte load waited for (all counters) before its value indexes the table
+        const int i00 = src[(int64_t)y0 * W + x0], i01 = src[(int64_t)y0 * W + x1];
+        const int i10 = src[(int64_t)y1 * W + x0], i11 = src[(int64_t)y1 * W + x1];
+        __builtin_amdgcn_s_waitcnt(0);
+        const float a00 = t[i00], a01 = t[i01], a10 = t[i10], a11 = t[i11];
+#else
         const float a00 = t[src[(int64_t)y0 * W + x0]];
         const float a01 = t[src[(int64_t)y0 * W + x1]];
         const float a10 = t[src[(int64_t)y1 * W + x0]];
         const float a11 = t[src[(int64_t)y1 * W + x1]];
+#endif
         v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
     }
     return f32x4{v[0], v[1], v[2], 0.f};
