@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--trials", type=int, default=8)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--n", type=int, default=2, help="instances in flight at once")
+    ap.add_argument("--ref-after", type=int, default=0, help="extra solo runs before the reference is taken")
     ap.add_argument("--detail", default="", help="buffer name prefix to describe when it differs (count, max |diff|, where)")
     ap.add_argument("--stem-debug", action="store_true",
                     help="a -DSTEM_TABLE_DEBUG build (EDGEDET_LIB): print its table-stem LDS check counters per trial")
@@ -52,6 +53,9 @@ def main():
     bufs = sorted(plans[0].buffers.values(), key=lambda b: b.off)
     go(0)
     torch.cuda.synchronize()
+    for _ in range(a.ref_after):
+        go(0)
+        torch.cuda.synchronize()
     ref = {b.name: b.tensor().clone() for b in bufs}
     ref_host = {b.name: ref[b.name].cpu() for b in bufs}  # to tell a changed reference copy from a changed buffer
     if a.stem_debug:
