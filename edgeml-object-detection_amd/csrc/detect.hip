@@ -341,15 +341,37 @@ __device__ __forceinline__ int block_sum_uniform(int wave_val, int* red) {
     return tot;
 }
 
+// count of keys >= t over one wave: one ballot + popcount per register, the popcounts summed in four
+// independent chains (written as one running sum, the compiler emits a serial chain of dependent
+// s_add, which then sets a probe's latency; SEL_SERIAL_COUNT keeps that form for A/B builds)
+template <int PER>
+__device__ __forceinline__ int wave_count_ge(const uint32_t (&kr)[PER], uint32_t t) {
+#ifdef SEL_SERIAL_COUNT
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) n += __popcll(__ballot(kr[j] >= t));
+    return n;
+#else
+    int n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j += 4) {
+        n0 += __popcll(__ballot(kr[j] >= t));
+        if (j + 1 < PER) n1 += __popcll(__ballot(kr[j + 1] >= t));
+        if (j + 2 < PER) n2 += __popcll(__ballot(kr[j + 2] >= t));
+        if (j + 3 < PER) n3 += __popcll(__ballot(kr[j + 3] >= t));
+        asm volatile("" : "+s"(n0), "+s"(n1), "+s"(n2), "+s"(n3));  // keeps the four chains apart
+    }
+    return (n0 + n1) + (n2 + n3);
+#endif
+}
+
 // count of keys >= t over the block.  red holds 2 x NW slots used alternately by successive calls
 // (`parity`), so one barrier per probe suffices: a wave cannot rewrite a slot set before every wave
 // has passed the barrier that follows the next probe's write.
 template <int NT, int PER>
 __device__ __forceinline__ int count_ge(const uint32_t (&kr)[PER], uint32_t t, int* red, int& parity) {
     constexpr int NW = NT / 64;
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) c += __popcll(__ballot(kr[j] >= t));
+    const int c = wave_count_ge<PER>(kr, t);
     int* r = red + parity * NW;
     parity ^= 1;
     if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = c;
@@ -360,20 +382,27 @@ __device__ __forceinline__ int count_ge(const uint32_t (&kr)[PER], uint32_t t, i
     return tot;
 }
 
+// block min of the valid (nonzero) keys and block max, in one exchange (2 x NW slots of red)
 template <int NT>
-__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, int* red) {
+__device__ __forceinline__ void block_minmax_u32(uint32_t& mn, uint32_t& mx, int* red) {
+    constexpr int NW = NT / 64;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
-        v = u > v ? u : v;
+        const uint32_t a = (uint32_t)__shfl_xor((int)mn, o), b = (uint32_t)__shfl_xor((int)mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
     }
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (int)v;
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = (int)mn;
+        red[NW + (threadIdx.x >> 6)] = (int)mx;
+    }
     __syncthreads();
-    uint32_t m = 0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) m = (uint32_t)red[w] > m ? (uint32_t)red[w] : m;
+    for (int w = 0; w < NW; ++w) {
+        mn = (uint32_t)red[w] < mn ? (uint32_t)red[w] : mn;
+        mx = (uint32_t)red[NW + w] > mx ? (uint32_t)red[NW + w] : mx;
+    }
     __syncthreads();
-    return m;
 }
 
 // kmin < K relaxes the selection to "some prefix of the order": the bisection stops at the first
@@ -389,11 +418,15 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
     int need_eq = 0;
     const bool take_all = nvalid <= K;
     if (!take_all) {
-        uint32_t km = 0;
+        uint32_t kmn = 0xffffffffu, kmx = 0u;
 #pragma unroll
-        for (int j = 0; j < PER; ++j) km = kr[j] > km ? kr[j] : km;
-        // bisection on [1, max + 1): count(>= lo) >= K > count(>= hi)
-        uint64_t lo = 1, hi = (uint64_t)block_max_u32<NT>(km, red + 2 * (NT / 64)) + 1;
+        for (int j = 0; j < PER; ++j) {
+            kmn = kr[j] != 0u && kr[j] < kmn ? kr[j] : kmn;
+            kmx = kr[j] > kmx ? kr[j] : kmx;
+        }
+        block_minmax_u32<NT>(kmn, kmx, red + 2 * (NT / 64));  // red: 4 x NW slots
+        // bisection on [min, max + 1): count(>= lo) >= K > count(>= hi)  (count(>= min) = nvalid > K)
+        uint64_t lo = kmn, hi = (uint64_t)kmx + 1;
         bool prefix = false;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
@@ -780,12 +813,7 @@ __device__ __forceinline__ int wave_select_topk(const float* __restrict__ sc, in
         const float v = sc[i < A ? i : A - 1];
         kr[j] = (i < A && v > score_thresh) ? __float_as_uint(v) : 0u;  // probabilities >= 0: bits ordered
     }
-    auto count_ge = [&](uint32_t t) -> int {
-        int n = 0;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) n += __popcll(__ballot(kr[j] >= t));
-        return n;
-    };
+    auto count_ge = [&](uint32_t t) -> int { return wave_count_ge<PER>(kr, t); };
     const int nvalid = count_ge(1u);
     const bool take_all = nvalid <= topk;
     uint32_t T = 1u;
@@ -952,6 +980,146 @@ __global__ void __launch_bounds__(256) ssd_class_select_kernel(const float* __re
                                                   }
                                               });
     for (int t = (written < topk ? written : topk) + lane; t < topk; t += 64) pk[t] = 0u;
+}
+
+// Stage 1, block form (the default): NW waves per (image, class), wave w holding elements
+// i = lane + 64*(w*PW + j).  The one-wave form above issues ~7,000 dependent instructions per wave
+// at ~1.4 waves per SIMD (profiles/r5h_ssd_sq_stall.txt: issue-bound, 34 us); here each bisection
+// probe is NW partial ballot counts summed through LDS (double-buffered: one barrier per probe), and
+// the compaction offsets each wave by the counts of the waves before it, so the pool is the one the
+// wave form writes, slot for slot.
+constexpr int SEL_PW = 13;  // 4 waves x 13 registers x 64 lanes = 3,328 anchors, the wave form's limit
+
+template <int NW, int PW>
+__global__ void __launch_bounds__(64 * NW) ssd_class_select_block_kernel(const float* __restrict__ scores_t, int A,
+                                                                         int NC, float score_thresh, int topk,
+                                                                         uint32_t* __restrict__ pool_key,
+                                                                         int* __restrict__ pool_ref) {
+    __shared__ int red[2][NW];
+    __shared__ uint32_t kmn_s[NW], kmx_s[NW];
+    __shared__ int ng_s[NW], ne_s[NW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const int c = blockIdx.x + 1;  // class 0 is background
+    const int b = blockIdx.y;
+    const int64_t base = ((int64_t)b * (NC - 1) + (c - 1)) * topk;
+    uint32_t* pk = pool_key + base;
+    int* pr = pool_ref + base;
+    const float* sc = scores_t + ((int64_t)b * NC + c) * A;
+    uint32_t kr[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int i = lane + 64 * (w * PW + j);
+        const float v = sc[i < A ? i : A - 1];  // clamped: all PW loads in flight at once
+        kr[j] = (i < A && v > score_thresh) ? __float_as_uint(v) : 0u;
+    }
+    int par = 0;
+    auto count_ge = [&](uint32_t t) -> int {
+        const int n = wave_count_ge<PW>(kr, t);
+        if (lane == 0) red[par][w] = n;
+        __syncthreads();
+        int s = 0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += red[par][v];
+        par ^= 1;
+        return s;
+    };
+    const int nvalid = count_ge(1u);
+    const bool take_all = nvalid <= topk;
+    uint32_t T = 1u;
+    int need_eq = 0;
+    if (!take_all) {
+        uint32_t kmn = 0xffffffffu, kmx = 0u;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            kmn = kr[j] != 0u && kr[j] < kmn ? kr[j] : kmn;
+            kmx = kr[j] > kmx ? kr[j] : kmx;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t a = (uint32_t)__shfl_xor((int)kmn, o), bb = (uint32_t)__shfl_xor((int)kmx, o);
+            kmn = a < kmn ? a : kmn;
+            kmx = bb > kmx ? bb : kmx;
+        }
+        if (lane == 0) {
+            kmn_s[w] = kmn;
+            kmx_s[w] = kmx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+            kmn = kmn_s[v] < kmn ? kmn_s[v] : kmn;
+            kmx = kmx_s[v] > kmx ? kmx_s[v] : kmx;
+        }
+        // the same bisection as the wave form: count(>= lo) >= topk > count(>= hi)
+        uint64_t lo = kmn, hi = (uint64_t)kmx + 1;
+        int chi = 0;
+        while (hi - lo > 1) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            const int cnt = count_ge((uint32_t)mid);
+            if (cnt >= topk) {
+                lo = mid;
+            } else {
+                hi = mid;
+                chi = cnt;
+            }
+        }
+        T = (uint32_t)lo;
+        need_eq = topk - chi;
+    }
+    // this wave's candidates above / at the threshold, then its offsets in index order
+    int ngw = 0, new_ = 0;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const uint32_t k = kr[j];
+        ngw += __popcll(__ballot(take_all ? (k != 0u) : (k > T)));
+        new_ += __popcll(__ballot(!take_all && k == T));
+    }
+    if (lane == 0) {
+        ng_s[w] = ngw;
+        ne_s[w] = new_;
+    }
+    __syncthreads();
+    int pg = 0, pe = 0, tg = 0, te = 0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+        if (v < w) {
+            pg += ng_s[v];
+            pe += ne_s[v];
+        }
+        tg += ng_s[v];
+        te += ne_s[v];
+    }
+    int eq_taken = pe < need_eq ? pe : need_eq;
+    int written = pg + eq_taken;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const uint32_t k = kr[j];
+        const bool gt = take_all ? (k != 0u) : (k > T);
+        const bool eq = !take_all && k == T;
+        const unsigned long long mg = __ballot(gt), me = __ballot(eq);
+        const int ng = __popcll(mg), ne = __popcll(me);
+        const int budget = need_eq - eq_taken;
+        const int i = lane + 64 * (w * PW + j);
+        if (gt) {
+            const int slot = written + __popcll(mg & lt_mask);
+            pk[slot] = k;
+            pr[slot] = i;
+        }
+        if (eq) {
+            const int q = __popcll(me & lt_mask);
+            if (q < budget) {
+                const int slot = written + ng + q;
+                pk[slot] = k;
+                pr[slot] = i;
+            }
+        }
+        const int used = ne < budget ? ne : (budget > 0 ? budget : 0);
+        written += ng + used;
+        eq_taken += used;
+    }
+    const int total = tg + (te < need_eq ? te : need_eq);
+    for (int t = total + threadIdx.x; t < topk; t += 64 * NW) pk[t] = 0u;
 }
 
 // Stage 2, ssd_image_nms_kernel: one workgroup per image.  The pool's keys live in VGPRs (element
@@ -1942,8 +2110,16 @@ int ssd_postprocess_launch(const SsdPostParams& P, hipStream_t s) {
     EDGEDET_REQUIRE(P.topk > 0 && (int64_t)(P.NC - 1) * P.topk <= (int64_t)NT * PER,
                     "ssd_postprocess: (classes-1) * topk must be <= 27648");
     EDGEDET_REQUIRE(P.N > 0 && P.N + M <= KCAP, "ssd_postprocess: detections per image must be <= 1024");
-    hipLaunchKernelGGL(ssd_class_select_kernel<PER_A>, dim3((unsigned)cdiv(P.NC - 1, 4), P.B), dim3(256), 0, s,
-                       P.scores_t, P.A, P.NC, P.score_thresh, P.topk, P.pool_key, P.pool_ref);
+    if (P.select_wave) {
+        hipLaunchKernelGGL(ssd_class_select_kernel<PER_A>, dim3((unsigned)cdiv(P.NC - 1, 4), P.B), dim3(256), 0, s,
+                           P.scores_t, P.A, P.NC, P.score_thresh, P.topk, P.pool_key, P.pool_ref);
+    } else {
+        constexpr int NWS = 4;
+        static_assert(NWS * SEL_PW >= PER_A, "the block form covers the wave form's anchors");
+        hipLaunchKernelGGL((ssd_class_select_block_kernel<NWS, SEL_PW>), dim3((unsigned)(P.NC - 1), P.B),
+                           dim3(64 * NWS), 0, s, P.scores_t, P.A, P.NC, P.score_thresh, P.topk, P.pool_key,
+                           P.pool_ref);
+    }
     EDGEDET_LAUNCH_CHECK();
     auto k = ssd_image_nms_kernel<NT, PER, M, KCAP>;
     const size_t lds = sizeof(ImgSmem<M, KCAP, NT * PER / 32>);

@@ -45,7 +45,8 @@
 //   BOX_CLASS_NMS  p0 scores; p1 boxes; p2 counts; p3..7 records; i0..3 B,R,NC,kmax;
 //                  f0 score_thresh; f1 min_size; d0 iou
 //   SSD_POSTPROCESS p0 scores_t; p1 boxes; p2 pool_key; p3 pool_ref; p4 ratio|0; p5 out_box; p6 out_score;
-//                  p7 out_label|0; p8 out_count; i0..4 B,A,NC,topk,N; f0 score_thresh; d0 iou
+//                  p7 out_label|0; p8 out_count; i0..4 B,A,NC,topk,N; i5 1 = one-wave class select;
+//                  f0 score_thresh; d0 iou
 //   GN_STATS       p0 x[B,HW,C]; p1 gamma; p2 beta; p3 scale[B,C]; p4 shift[B,C]; i0..3 B,HW,C,G; f0 eps
 //   RETINA_SELECT  p0 logits[B,Atot,K]; p1 deltas[B,Atot,4]; p2 anchors[Atot,4]; p3..7 records
 //                  (box,score,tb,label,count) [B,L,kmax]; i0..4 B,L,Atot,K,topk; i5 kmax; i6..10 a0 per level;
@@ -442,6 +443,7 @@ static int run_op(const edgedet_op& o, hipStream_t s) {
             p.NC = (int)I[2];
             p.topk = (int)I[3];
             p.N = (int)I[4];
+            p.select_wave = (int)I[5];
             p.score_thresh = o.f[0];
             p.iou = o.d[0];
             return ssd_postprocess_launch(p, s);

@@ -172,6 +172,7 @@ struct SsdPostParams {
     int64_t* out_label;     // [B][N] or null
     int* out_count;         // [B]
     int B, A, NC, topk, N;
+    int select_wave;        // 1: the one-wave-per-class selection (A/B form)
     float score_thresh;
     double iou;
 };

@@ -938,6 +938,7 @@ class SSDLite {
             o.name = "postprocess.nms" + sfx;
             const int64_t iv[5] = {B, A, NC, KM, DETS};
             for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
+            o.i[5] = env_int("EDGEDET_SSD_SELECT_WAVE", 0);
             o.p[0] = view(sh.scores_t);
             o.p[1] = view(sh.boxes);
             o.p[2] = P.ref(pk);

@@ -336,12 +336,15 @@ def dwconv2d_nhwc(x, w_taps, bias, k, stride, pad, act=None, se_part=False):
     return y, part
 
 
-def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ratio=None, path="image"):
+def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ratio=None, path="image",
+                    select="block", pool=False):
     """SSD.postprocess_detections tail on device buffers (per class score > t, top-k, batched NMS,
     [:dets]); scores_t [B, NC, A] class probabilities, boxes [B, A, 4] decoded + clipped.
 
     path="image" runs the SSD_POSTPROCESS record, path="class" the SSD_CLASS_NMS + MERGE_TOPK pair.
-    Returns (out_box [B, dets, 4] scaled by ratio [B, 2], out_score, out_label, out_count)."""
+    select="wave" runs the image path's class selection one wave per class (the A/B form).
+    Returns (out_box [B, dets, 4] scaled by ratio [B, 2], out_score, out_label, out_count), plus the
+    image path's candidate pool (key, anchor) [B, NC-1, topk] when pool=True."""
     _need_cuda(scores_t, boxes, ratio)
     B, NC, A = scores_t.shape
     dev = scores_t.device
@@ -355,7 +358,7 @@ def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ra
         pr = torch.empty((B, NC - 1, topk), dtype=torch.int32, device=dev)
         rec = np.zeros(1, dtype=OP_DTYPE)
         rec[0]["kind"] = SSD_POSTPROCESS
-        rec[0]["i"][:5] = [B, A, NC, topk, dets]
+        rec[0]["i"][:6] = [B, A, NC, topk, dets, 1 if select == "wave" else 0]
         for j, t in enumerate((scores_t, boxes, pk, pr, ratio, ob, osc, olab, ocnt)):
             rec[0]["p"][j] = 0 if t is None else t.data_ptr()
         rec[0]["f"][0] = score_thresh
@@ -382,6 +385,8 @@ def ssd_postprocess(scores_t, boxes, topk, dets, score_thresh, iou_threshold, ra
         keep_alive += [rb, rs, rt, rl, rc]
     check(lib().edgedet_plan_run(rec.ctypes.data_as(ctypes.c_void_p), len(rec), stream_handle()))
     torch.cuda.current_stream().synchronize()
+    if pool and path == "image":
+        return ob, osc, olab, ocnt, pk, pr
     return ob, osc, olab, ocnt
 
 

@@ -124,3 +124,44 @@ def test_shapes_and_thresholds_exact(path, nc, a, topk, dets, thr):
     cnt = run_and_compare(st, bx, topk, dets, thr, 0.55, ratio, path)
     if thr >= 1.0:  # probabilities never exceed 1
         assert (cnt == 0).all()
+
+
+def _pools(st, bx, topk, dets, thr, select):
+    from edgeml_amd import ops
+    out = ops.ssd_postprocess(torch.from_numpy(st).cuda(), torch.from_numpy(bx).cuda(), topk, dets, thr, 0.55,
+                              None, path="image", select=select, pool=True)
+    return [t.cpu() for t in out]
+
+
+@pytest.mark.parametrize("case", ["random", "quantised", "all_equal", "max_anchors", "few_valid", "topk_gt_half"])
+def test_block_select_pool_equals_wave_select(case):
+    """The default class selection (four waves per class, counts summed through LDS) writes the same
+    candidate pool, slot for slot, as the one-wave form, and the same detections: ties at the top-k
+    threshold that span the waves' register ranges are taken lowest anchor first by both."""
+    rs = np.random.RandomState(11)
+    B, NC, A, topk, thr = 2, 91, 3234, 300, 0.001
+    if case == "random":
+        st = _softmax(rs.normal(0, 2, (B, NC, A)).astype(np.float32))
+    elif case == "quantised":
+        st = _softmax(rs.normal(0, 2, (B, NC, A)).astype(np.float32))
+        st = (np.floor(st * 4 * NC) / (4 * NC)).astype(np.float32)
+    elif case == "all_equal":  # every key ties: the threshold's equal run covers all four waves
+        st = np.full((B, NC, A), 1.0 / NC, np.float32)
+    elif case == "max_anchors":
+        A = 64 * 52
+        st = _softmax(rs.normal(0, 2, (B, NC, A)).astype(np.float32))
+    elif case == "few_valid":  # take-all path, and classes with no candidate
+        st = _softmax(rs.normal(0, 3, (B, NC, A)).astype(np.float32))
+        thr = 0.3
+    else:  # most anchors kept: the threshold sits low, ties in the last wave's range
+        NC, A, topk = 21, 500, 400
+        st = _softmax(rs.normal(0, 1, (B, NC, A)).astype(np.float32))
+        st = (np.round(st * 64) / 64).astype(np.float32)
+    bx = _boxes(rs, B, A, cluster=30)
+    a = _pools(st, bx, topk, 300, thr, "block")
+    b = _pools(st, bx, topk, 300, thr, "wave")
+    for x, y, name in zip(a, b, ("box", "score", "label", "count", "pool_key", "pool_ref")):
+        if name == "pool_ref":  # slots past the written count hold no anchor (key 0)
+            x = torch.where(a[4] != 0, x, -1)
+            y = torch.where(b[4] != 0, y, -1)
+        assert torch.equal(x, y), (case, name)
