@@ -426,7 +426,11 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
         }
         block_minmax_u32<NT>(kmn, kmx, red + 2 * (NT / 64));  // red: 4 x NW slots
         // bisection on [min, max + 1): count(>= lo) >= K > count(>= hi)  (count(>= min) = nvalid > K)
+#ifdef SEL_LO_ONE
+        uint64_t lo = 1, hi = (uint64_t)kmx + 1;  // A/B builds: the bisection from key 1
+#else
         uint64_t lo = kmn, hi = (uint64_t)kmx + 1;
+#endif
         bool prefix = false;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
