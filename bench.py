@@ -468,6 +468,9 @@ def attach_pipeline(roof, instances, steps):
     ach = work / (ms * 1e-3) / scale
     roof.update({"launch_ms": round(ms, 4), "achieved": round(ach, 2), "frac": round(ach / roof["peak"], 4),
                  "frac_in_pipeline": round(ach / roof["peak"], 4),
+                 "contention": "inclusive: launch_ms / achieved / frac are the launch's span inside the running "
+                               "pipeline, CU time held by the other chains' kernels included (what the kernel "
+                               "trace of the pipeline averages); the kernel alone against its roof is *_solo",
                  "timing": f"workgroup 0's start to the last workgroup's end on the GPU's 100 MHz clock, written by "
                            f"the kernel into a probe slot, {nlaunch} launches over {steps} pipelined passes of "
                            f"{len(instances)} instances ({ips:.1f} img/s with the probes); *_solo: the launch "
@@ -516,7 +519,7 @@ def pipeline_launch_ms(instances, k, steps):
                                        ctypes.byref(g)))
         for _ in range(2):  # prime, as plan.capture does
             O.check(L.edgedet_graph_launch(g, O.stream_handle(s)))
-        slots.append((p, s, d2h_buffers(p), g, dev, host, [False, False]))
+        slots.append((p, s, d2h_buffers(p), g, dev, host, [None, None]))
     torch.cuda.synchronize()
     ring, ticks = [], []
 
@@ -529,7 +532,7 @@ def pipeline_launch_ms(instances, k, steps):
             ring.pop(0).synchronize()
         p, s, d2h, g, dev, host, used = slots[j % n]
         v = (j // n) % 2
-        if used[v] and keep:  # this buffer's pass (2n passes back) has completed
+        if used[v] is True:  # this buffer's pass (2n passes back) has completed and was a timed one
             ticks.append(read(host, v))
         O.check(L.edgedet_graph_launch(g, O.stream_handle(s)))
         with torch.cuda.stream(s):
@@ -539,7 +542,7 @@ def pipeline_launch_ms(instances, k, steps):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(s)
         ring.append(ev)
-        used[v] = True
+        used[v] = keep  # readings of settle passes are never averaged
         return ev
     t0, j = time.perf_counter(), 0
     while time.perf_counter() - t0 < SETTLE_S or j < 4 * n:  # settle, as timed_steps
@@ -551,7 +554,7 @@ def pipeline_launch_ms(instances, k, steps):
     torch.cuda.synchronize()
     for _, _, _, _, _, host, used in slots:
         for v in range(2):
-            if used[v]:
+            if used[v] is True:
                 ticks.append(read(host, v))
     ips = steps * instances[0][0].B / (first.elapsed_time(last) / 1e3)
     for sl in slots:

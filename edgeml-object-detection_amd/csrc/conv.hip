@@ -302,18 +302,25 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_mfma_kernel(ConvParams p) {
                 bf[j][0] = *reinterpret_cast<const f32x4*>(src);
                 bf[j][1] = *reinterpret_cast<const f32x4*>(src + 4);
             }
+            // each tile's 16 K of this half stage into a stage sum from zero, then one add into the
+            // running output (the running sum is rounded once per 16 K instead of at every product)
+            // (the 2 x 2-tile forms, 128 x 128 and 256 x 128, run only under fp32 conv math and have no
+            // registers for four stage sums: they keep the plain fmaf chain, the accuracy reference of
+            // tools/accuracy_probe.py)
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const float a = (t < 4) ? af[i][0][t & 3] : af[i][1][t & 3];
+                for (int j = 0; j < TN; ++j) {
+                    floatx16 s{};
+                    if constexpr (TM * TN == 4) s = acc[i][j];
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) {
+                    for (int t = 0; t < 8; ++t) {
+                        const float a = (t < 4) ? af[i][0][t & 3] : af[i][1][t & 3];
                         const float b = (t < 4) ? bf[j][0][t & 3] : bf[j][1][t & 3];
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+                        s = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, s, 0, 0, 0);
                     }
+                    acc[i][j] = TM * TN == 4 ? s : acc[i][j] + s;
                 }
-            }
         }
         if (kc + 1 < nk) store_stage(buf ^ 1);
         __syncthreads();
@@ -362,16 +369,19 @@ __device__ __forceinline__ void pw_load(const ConvParams& p, PwFrag<TM, TN>& f, 
             f.b[j][q] = bval[j] ? *reinterpret_cast<const f32x4*>(brow[j] + kk + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// One 32-deep K chunk: each tile's chunk sum from zero, then one add into the running output.
 template <int TM, int TN>
 __device__ __forceinline__ void pw_mma(const PwFrag<TM, TN>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j) {
+            floatx16 s{};
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][t >> 2][t & 3], f.b[j][t >> 2][t & 3],
-                                                                  acc[i][j], 0, 0, 0);
+            for (int t = 0; t < 16; ++t)
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][t >> 2][t & 3], f.b[j][t >> 2][t & 3], s, 0, 0, 0);
+            acc[i][j] = acc[i][j] + s;
+        }
 }
 
 template <int TM, int TN>
@@ -596,7 +606,7 @@ __global__ void __launch_bounds__(256) pw_stream_kernel(ConvParams p, int ncg) {
 // MFMAs (8 x 64 cycles) per 32x32x16 block: 2.67x the fp32-MFMA rate at fp32-grade accuracy.
 //
 // Weights arrive pre-split as three bf16 planes w3[3][Cout][Kpad] (plan.py split_bf16x3; the same
-// RN split); activations are split once per block while staging (global fp32 -> registers ->
+// RN split, of -w in the odd 32-wide K blocks: the sign-alternated stages, conv_x6b_body); activations are split once per block while staging (global fp32 -> registers ->
 // three bf16 planes in LDS), so the split costs O(BM*K) VALU per block, not O(BM*BN*K).
 // LDS: K stage of 16, rows of 16 bf16 padded to 24 (48 B: the 16-lane b128 read groups hit 16
 // disjoint 4-bank groups), double-buffered through registers, one barrier per stage.
@@ -717,10 +727,12 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     struct Regs {
         f32x4 a[AJ];
         uint4 b[BJ];
+        float sg;  // the stage's sign (the split weights' odd 32-wide K blocks are negated, conv_x6b_body)
     };
     Regs r0, r1;
 
     auto load_stage = [&](Regs& R, int k0) {
+        R.sg = ((k0 >> 5) & 1) ? -1.f : 1.f;
         if constexpr (UT) {
             const int tap = (int)fdiv((uint32_t)k0, p.div_cin);
             const int ci = k0 - tap * p.Cin + c4 * 4;
@@ -760,9 +772,14 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
             R.b[j] = (BL % NT == 0 || tid + NT * j < BL) ? *reinterpret_cast<const uint4*>(b_row[j] + k0)
                                                        : uint4{0u, 0u, 0u, 0u};  // rows past Cout: row 0
     };
+    float sgb0 = 1.f, sgb1 = 1.f;
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
+        if (buf)
+            sgb1 = R.sg;
+        else
+            sgb0 = R.sg;
 #pragma unroll
         for (int j = 0; j < AJ; ++j) {
             const int row = (tid >> 2) + (NT / 4) * j;
@@ -794,6 +811,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
     auto compute = [&](int buf) {
         const unsigned short* A = As + buf * 3 * PA;
         const unsigned short* Bb = Bs + buf * 3 * PB;
+        const float sg = buf ? sgb1 : sgb0;
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -805,17 +823,20 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_x6_kernel(ConvParams p) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
                 bfr[j][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + (wave_n * TN * 32 + j * 32 + l32) * LDR6 + 8 * h);
-        // smallest terms first: (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
+        // the stage's six split products, smallest first, into a stage sum that starts at zero, then
+        // one fp32 add into the running output (the error structure of conv_x6b_body's mfma16)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], acc[i][j], 0, 0, 0);
+                floatx16 s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][2], bfr[j][0], floatx16{}, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][1], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][2], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][1], bfr[j][0], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][1], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][0], bfr[j][0], s, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_fmaf(sg, s[r], acc[i][j][r]);
             }
     };
     load_stage(r0, 0);
@@ -844,6 +865,15 @@ constexpr int X3Z = 32;  // leading zero elements of a pre-split scratch (16-B a
 __device__ __forceinline__ int swz_key(int row) { return (row >> 2) & 2; }
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ swz_key(row)); }
 
+#ifndef X6_SLEEP
+#define X6_SLEEP 0
+#endif
+#ifndef X6_SB
+#define X6_SB 0
+#endif
+#ifndef X6_FRESH
+#define X6_FRESH 0
+#endif
 // XF: the input transform is active (SE scale / GN shift / ReLU); UT: Cin % 32 == 0, so every stage
 // lies inside one filter tap and the tap decomposition is wave-uniform (scalar) work.
 // PS: the input arrives pre-split (p.x3: three dense bf16 planes written by split_act_kernel, input
@@ -943,6 +973,7 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
         f32x4 a[PS ? 1 : AJ];
         uint4 a3[PS ? AJ : 1][3];
         uint4 b[3];
+        float sg;  // the stage's sign (sign-alternated stages, below)
     };
     const int64_t x3plane = (int64_t)p.B * p.H * p.W * p.Cin;
     // x3 scratch: X3Z zero elements (the source of padding taps under LDS-DMA), then the three planes
@@ -960,6 +991,7 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
     };
     auto load_stage = [&](Regs& R, const StageK& sk, int bbuf) {
         const int k0 = sk.k0;
+        R.sg = ((k0 >> 5) & 1) ? -1.f : 1.f;  // the sign the split weights carry for this K block
         if constexpr (GL) {
             // B by LDS-DMA: wave w copies rows rb + 16w .. rb + 16w + 15 of each plane for every 128-row
             // block rb (1 KiB per instruction, lane l -> the 16-B slot l of the block); the swizzle is
@@ -1063,9 +1095,20 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
                 R.b[pl] = b_ok ? *reinterpret_cast<const uint4*>(b_src + pl * wplane + k0) : uint4{0u, 0u, 0u, 0u};
         }
     };
+    // Sign-alternated stages: the split weight planes hold -w in every odd 32-wide K block
+    // (split_bf16x3_kernel), so those stages' sums come out negated and are subtracted.  The matrix
+    // core aligns each lane group's 8 products to the largest and truncates the rest toward -inf
+    // (a 22-bit window, fitted to tools/accuracy_probe.py), a bias that grows with K; on negated
+    // stages the same truncation rounds the other way, so over the stages it cancels.
+    // sgb<buf>: the sign of the stage held in LDS buffer buf.
+    float sgb0 = 1.f, sgb1 = 1.f;
     auto store_stage = [&](const Regs& R, int buf) {
         unsigned short* A = As + buf * 3 * PA;
         unsigned short* Bb = Bs + buf * 3 * PB;
+        if (buf)
+            sgb1 = R.sg;
+        else
+            sgb0 = R.sg;
         if constexpr (PS && GL) {
             // A arrived by LDS-DMA
         } else if constexpr (PS) {
@@ -1164,20 +1207,54 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
             for (int pl = 0; pl < 3; ++pl) F.b[u][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
         }
     };
-    // quadrant (ha, hb) from the A half in FA and the B half in FB; smallest terms first:
-    // (a2b0 + a1b1 + a0b2) + (a1b0 + a0b1) + a0b0
-    auto mfma16 = [&](const F16& FA, const F16& FB, int ha, int hb) {
+    // quadrant (ha, hb) from the A half in FA and the B half in FB.  The stage's six split products
+    // (smallest first: a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0) chain into a fresh stage sum that
+    // starts at zero, and the running output takes that sum with ONE fp32 add (stage_add): each MFMA
+    // rounds its lane-group partial sums into C one group at a time, so chaining the six terms into
+    // the running output rounded it 24 times per stage at its full magnitude; the stage sum takes
+    // those roundings at the stage's (K/32 times smaller) magnitude.  RMS error against float64 on
+    // the 3x3 256->256 conv 1.39e-7 -> about 3e-8, below torch's CPU conv.
+    // A tile's stage-sum add is issued after the NEXT tile's six MFMAs (pend), so the MFMA result it
+    // reads has landed and no wait states separate them; flush() adds the last pending one.
+    struct Pend {
+        f32x4 v;
+        float sg;
+        int i, j;  // acc4 tile, -1: none (constants after unrolling)
+    } pend{f32x4{0.f, 0.f, 0.f, 0.f}, 1.f, -1, -1};
+    auto flush = [&]() {
+        if (pend.i >= 0) {
+#if X6_FRESH == 1
+            acc4[pend.i][pend.j] = pend.v;  // timing experiment only: no add (wrong results)
+#else
+#pragma unroll
+            for (int r = 0; r < 4; ++r)  // c +- s, one rounding
+                acc4[pend.i][pend.j][r] = __builtin_fmaf(pend.sg, pend.v[r], acc4[pend.i][pend.j][r]);
+#endif
+        }
+        pend.i = -1;
+    };
+    auto mfma16 = [&](const F16& FA, const F16& FB, int ha, int hb, float sg) {
 #pragma unroll
         for (int t = 0; t < TM; ++t)
 #pragma unroll
             for (int u = 0; u < TN; ++u) {
-                f32x4& c = acc4[ha * TM + t][hb * TN + u];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][2], FB.b[u][0], c, 0, 0, 0);
+#if X6_FRESH == 2
+                f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][2], FB.b[u][0], acc4[ha * TM + t][hb * TN + u],
+                                                                  0, 0, 0);  // timing experiment: the old chain
+#else
+                f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][2], FB.b[u][0], f32x4{0.f, 0.f, 0.f, 0.f},
+                                                                  0, 0, 0);
+#endif
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][1], FB.b[u][1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][2], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][1], FB.b[u][0], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][0], c, 0, 0, 0);
+#if X6_SB
+                __builtin_amdgcn_sched_barrier(X6_SB);  // the previous tile's add stays behind this chain
+#endif
+                flush();
+                pend = Pend{c, sg, ha * TM + t, hb * TN + u};
             }
     };
     // static priority for waves 4..7, the arbitration losers of a two-waves-per-SIMD block
@@ -1194,26 +1271,34 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
         if (nk > 1) load_stage(r0, next_k(ca), 1);
         read16(F0, 0, 0);
         read16(F1, 0, 1);
-        mfma16(F0, F0, 0, 0);
-        mfma16(F0, F1, 0, 1);
-        mfma16(F1, F0, 1, 0);
+        float sgc = sgb0;  // the sign of the stage in F0 / F1 (F1's quadrant (1, 1) is carried)
+        mfma16(F0, F0, 0, 0, sgc);
+        mfma16(F0, F1, 0, 1, sgc);
+        mfma16(F1, F0, 1, 0, sgc);
         if (nk > 1) store_stage(r0, 1);
+        flush();
         __syncthreads();
         for (int kc = 1; kc < nk; ++kc) {
             const int buf = kc & 1;
             if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
             read16(F0, buf, 0);
             __builtin_amdgcn_sched_barrier(0);  // issue the reads before the carried quadrant that hides them
-            mfma16(F1, F1, 1, 1);
+#if X6_SLEEP
+            if (wid >= 4) __builtin_amdgcn_s_sleep(X6_SLEEP);
+#endif
+            mfma16(F1, F1, 1, 1, sgc);
             __builtin_amdgcn_sched_barrier(0);  // F1 is rewritten only after the carried quadrant issued
+            sgc = buf ? sgb1 : sgb0;
             read16(F1, buf, 1);
-            mfma16(F0, F0, 0, 0);
-            mfma16(F0, F1, 0, 1);
-            mfma16(F1, F0, 1, 0);
+            mfma16(F0, F0, 0, 0, sgc);
+            mfma16(F0, F1, 0, 1, sgc);
+            mfma16(F1, F0, 1, 0, sgc);
             store_stage(r0, buf ^ 1);  // on the last stage a dead write of the idle buffer
+            flush();
             // Spread the split VALU, the LDS writes of stage k+1 and the fragment reads over the gaps
             // of the MFMAs (1 MFMA : 1 LDS read : 3 VALU : 1 LDS write; 0 groups cost FRCNN 3%, 1..5
             // VALU within 1%) instead of letting them bunch up after the last MFMA.
+#ifndef X6_NOSGB
 #pragma unroll
             for (int i = 0; i < TM * TN * 18; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -1221,9 +1306,11 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
                 __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
             }
+#endif
             __syncthreads();
         }
-        mfma16(F1, F1, 1, 1);
+        mfma16(F1, F1, 1, 1, sgc);
+        flush();
     } else {
         // Two register stages: stage k+2's global loads are issued before stage k's MFMAs, stage k+1's
         // (issued one stage earlier) are stored to LDS after them, so each load has two stages of MFMA
@@ -1238,11 +1325,13 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
             F16 F0, F1;
             read16(F0, kc & 1, 0);
             read16(F1, kc & 1, 1);
-            mfma16(F0, F0, 0, 0);
-            mfma16(F0, F1, 0, 1);
-            mfma16(F1, F0, 1, 0);
-            mfma16(F1, F1, 1, 1);
+            const float sgc = (kc & 1) ? sgb1 : sgb0;
+            mfma16(F0, F0, 0, 0, sgc);
+            mfma16(F0, F1, 0, 1, sgc);
+            mfma16(F1, F0, 1, 0, sgc);
+            mfma16(F1, F1, 1, 1, sgc);
             if (kc + 1 < nk) store_stage(hold, (kc & 1) ^ 1);
+            flush();
             __syncthreads();
         };
         for (int kc = 0; kc < nk; kc += 2) {
@@ -1396,10 +1485,11 @@ static int launch_x6b_group(ConvGroup& g, hipStream_t s) {
 
 // Device-side weight split (the same RN three-term split as plan.py split_bf16x3): w[n] fp32 ->
 // out[3][n] bf16 planes.
-__global__ void split_bf16x3_kernel(const float* __restrict__ w, int64_t n, unsigned short* __restrict__ out) {
+__global__ void split_bf16x3_kernel(const float* __restrict__ w, int64_t n, int64_t kpad,
+                                    unsigned short* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float x = w[i];
+    const float x = (((i % kpad) >> 5) & 1) ? -w[i] : w[i];  // odd 32-wide K blocks negated
     const __bf16 x0 = (__bf16)x;
     const float r1 = x - (float)x0;
     const __bf16 x1 = (__bf16)r1;
@@ -1655,10 +1745,11 @@ extern "C" int64_t edgedet_conv_weight_k(int32_t KH, int32_t KW, int64_t Cin) {
     return cdiv((int64_t)KH * KW * Cin, BK) * BK;
 }
 
-extern "C" int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream) {
+extern "C" int edgedet_split_bf16x3(const float* w, int64_t n, int64_t kpad, uint16_t* out, void* stream) {
     EDGEDET_REQUIRE(w && out && n > 0, "split_bf16x3: null pointer or empty");
+    EDGEDET_REQUIRE(kpad > 0 && kpad % BK6B == 0 && n % kpad == 0, "split_bf16x3: rows of kpad, a multiple of 32");
     hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, w, n,
-                       reinterpret_cast<unsigned short*>(out));
+                       kpad, reinterpret_cast<unsigned short*>(out));
     EDGEDET_LAUNCH_CHECK();
     return 0;
 }

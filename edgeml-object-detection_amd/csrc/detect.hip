@@ -343,15 +343,9 @@ __device__ __forceinline__ int block_sum_uniform(int wave_val, int* red) {
 
 // count of keys >= t over one wave: one ballot + popcount per register, the popcounts summed in four
 // independent chains (written as one running sum, the compiler emits a serial chain of dependent
-// s_add, which then sets a probe's latency; SEL_SERIAL_COUNT keeps that form for A/B builds)
+// s_add, which then sets a probe's latency)
 template <int PER>
 __device__ __forceinline__ int wave_count_ge(const uint32_t (&kr)[PER], uint32_t t) {
-#ifdef SEL_SERIAL_COUNT
-    int n = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) n += __popcll(__ballot(kr[j] >= t));
-    return n;
-#else
     int n0 = 0, n1 = 0, n2 = 0, n3 = 0;
 #pragma unroll
     for (int j = 0; j < PER; j += 4) {
@@ -362,7 +356,6 @@ __device__ __forceinline__ int wave_count_ge(const uint32_t (&kr)[PER], uint32_t
         asm volatile("" : "+s"(n0), "+s"(n1), "+s"(n2), "+s"(n3));  // keeps the four chains apart
     }
     return (n0 + n1) + (n2 + n3);
-#endif
 }
 
 // count of keys >= t over the block.  red holds 2 x NW slots used alternately by successive calls
@@ -408,9 +401,11 @@ __device__ __forceinline__ void block_minmax_u32(uint32_t& mn, uint32_t& mx, int
 // kmin < K relaxes the selection to "some prefix of the order": the bisection stops at the first
 // probe t with kmin <= count(>= t) <= K and every key >= t is taken (ties whole), which is all a
 // caller that consumes candidates in global order, round by round, needs.
-template <int NT, int PER>
+// red: 4 x NT / 64 slots (2 x NW for the double-buffered counts, 2 x NW for block_minmax_u32).
+template <int NT, int PER, int NR>
 __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsigned long long* keys, int* wsum,
-                                int* red, bool all_ties = false, int kmin = -1, int* nvalid_out = nullptr) {
+                                int (&red)[NR], bool all_ties = false, int kmin = -1, int* nvalid_out = nullptr) {
+    static_assert(NR >= 4 * (NT / 64), "select_topk_regs: red needs 4 x NT / 64 slots");
     int parity = 0;
     const int nvalid = count_ge<NT, PER>(kr, 1u, red, parity);
     if (nvalid_out) *nvalid_out = nvalid;
@@ -426,11 +421,7 @@ __device__ int select_topk_regs(const uint32_t (&kr)[PER], int K, int cap, unsig
         }
         block_minmax_u32<NT>(kmn, kmx, red + 2 * (NT / 64));  // red: 4 x NW slots
         // bisection on [min, max + 1): count(>= lo) >= K > count(>= hi)  (count(>= min) = nvalid > K)
-#ifdef SEL_LO_ONE
-        uint64_t lo = 1, hi = (uint64_t)kmx + 1;  // A/B builds: the bisection from key 1
-#else
         uint64_t lo = kmn, hi = (uint64_t)kmx + 1;
-#endif
         bool prefix = false;
         while (hi - lo > 1) {
             const uint64_t mid = lo + ((hi - lo) >> 1);
@@ -668,9 +659,6 @@ __device__ __forceinline__ bool iou_gt(f32x4 a, float area_a, f32x4 b, float are
 }
 
 // unrolled 8: overlaps the LDS reads of consecutive boxes j (RPN level-0 NMS 758k -> 715k cycles)
-#ifndef NMS_UNROLL
-#define NMS_UNROLL 8
-#endif
 // Greedy NMS over S.box[0..m) in sorted order.  In: S.valid = candidate may be kept (invalid ones
 // neither survive nor suppress).  Out: S.valid = kept.  If `groups`, only pairs with equal
 // S.aux[] group ids interact (batched_nms).
@@ -741,7 +729,7 @@ __device__ __forceinline__ unsigned long long nms_mask_word(const f32x4* bx, con
     const int gi = grp ? grp[i] : 0;
     const int j0 = w * 64;
     const int jend = min(m, j0 + 64);
-#pragma unroll NMS_UNROLL
+#pragma unroll 8
     for (int j = max(j0, i + 1); j < jend; ++j) {
         if (grp && grp[j] != gi) continue;
         const f32x4 bj = bx[j];
@@ -1194,18 +1182,10 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
         rh = ratio[2 * b + 1];
     }
     int total = 0;
-#ifdef NMS_PROFILE
-    long long t_sel = 0, t_sort = 0, t_nms = 0, t_out = 0, tp = __builtin_amdgcn_s_memtime();
-    int rounds = 0;
-#define NMS_STAMP(acc) do { const long long tn = __builtin_amdgcn_s_memtime(); acc += tn - tp; tp = tn; } while (0)
-#else
-#define NMS_STAMP(acc) do { } while (0)
-#endif
     while (true) {
         // any prefix of the global order between 3M/4 and M candidates serves a round
         int nleft;
         const int m = select_topk_regs<NT, PER>(kr, M, M, S.keys, S.wsum, S.red, false, 3 * M / 4, &nleft);
-        NMS_STAMP(t_sel);
         if (m == 0) break;
         if (tid < m) {
             const int i = key_index(S.keys[tid]);
@@ -1218,7 +1198,6 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             if (kr[j] && ((S.done[i >> 5] >> (i & 31)) & 1u)) kr[j] = 0u;
         }
         rank_sort_desc<NT>(S.keys, S.run, m);
-        NMS_STAMP(t_sort);
         // each candidate's class and its rank among the earlier sorted candidates of its class: within
         // the wave by a ballot per distinct class (ordered by lane), across waves by the per-wave class
         // counts; the class histogram is their sum
@@ -1409,7 +1388,6 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             }
         }
         __syncthreads();
-        NMS_STAMP(t_nms);
         const bool kf = tid < m && S.kflag[tid];
         int tot;
         const int pos = BlockScan<NT>::exclusive(kf ? 1 : 0, S.wsum, tot);
@@ -1425,18 +1403,9 @@ __global__ void __launch_bounds__(NT) ssd_image_nms_kernel(const uint32_t* __res
             if (out_label) out_label[o] = (int64_t)(S.cls[tid] + 1);
         }
         total += tot;
-        NMS_STAMP(t_out);
-#ifdef NMS_PROFILE
-        ++rounds;
-#endif
         if (total >= N || m >= nleft) break;  // a round may be a prefix shorter than M
     }
     if (tid == 0) out_count[b] = total < N ? total : N;
-#ifdef NMS_PROFILE
-    if (tid == 0 && b == 0)
-        printf("nms img0: rounds %d total %d select %lld sort %lld nms %lld out %lld (s_memtime ticks)\n", rounds, total,
-               t_sel, t_sort, t_nms, t_out);
-#endif
 }
 
 // ================================================================ RPN per-level selection
@@ -1505,19 +1474,10 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
         return r < cc[ch];
     };
     auto level_index = [&](int i) { return chunked ? ci[i] : i; };
-#ifdef RPN_PROFILE
-    long long tp = __builtin_amdgcn_s_memtime(), t_sel = 0, t_cmp = 0, t_sort = 0, t_dec = 0, t_nms = 0;
-#define RPN_STAMP(acc) do { __syncthreads(); const long long tn = __builtin_amdgcn_s_memtime(); acc += tn - tp; tp = tn; } while (0)
-#else
-#define RPN_STAMP(acc) do { } while (0)
-#endif
     const uint32_t T = radix_select<NT>(n, P.topk, fkey, S.hist, S.misc);
-    RPN_STAMP(t_sel);
     const bool take_all = S.misc[1] <= P.topk;
     const int m = compact<NT>(n, T, take_all, S.misc[5], KC, fkey, S.keys, S.wsum);
-    RPN_STAMP(t_cmp);
     bitonic_desc<NT>(S.keys, nullptr, m);
-    RPN_STAMP(t_sort);
     for (int t = threadIdx.x; t < m; t += NT) {
         const int i = level_index(key_index(S.keys[t]));
         const f32x4 d = db[i];
@@ -1529,14 +1489,7 @@ __global__ void __launch_bounds__(NT) rpn_level_nms_kernel(RpnParams P, SegOut o
         S.valid[t] = ((bx.z - bx.x) >= P.min_size && (bx.w - bx.y) >= P.min_size && score >= P.score_thresh) ? 1 : 0;
     }
     __syncthreads();
-    RPN_STAMP(t_dec);
     nms_block<NT, KC>(S, m, P.iou, false);
-    RPN_STAMP(t_nms);
-#ifdef RPN_PROFILE
-    if (threadIdx.x == 0 && b == 0)
-        printf("rpn level %d n %d: select %lld compact %lld sort %lld decode %lld nms %lld\n", l, L.n, t_sel, t_cmp,
-               t_sort, t_dec, t_nms);
-#endif
     write_kept<NT, KC>(S, m, b * P.nlevels + l, out, [&](int t, int64_t o) {
         const float logit = key_float((uint32_t)(S.keys[t] >> 32));
         out.box[o] = S.box[t];
@@ -1688,20 +1641,37 @@ __global__ void __launch_bounds__(NT) rpn_level_scan_kernel(RpnParams P, RpnSpli
     const int seg = b * P.nlevels + l;
     const int m = X.m[seg];
     const unsigned long long* gm = X.mask + (int64_t)seg * KC * NWORDS;
-    // rows i < m as 16-byte pairs of words, eight loads of each thread in flight before its stores (the
-    // words below a row's own block were never written and are never read)
+    // exactly the words rpn_mask_kernel wrote: rows i < m, words i / 64 .. nw - 1 (nothing below a
+    // row's own 64-row block, nothing past the last block).  Wave k stages row blocks k and
+    // 2 NW - 1 - k (17 row-block widths per wave), lane-contiguous within each block's
+    // rows x words, every load of the wave in flight before its stores.
     {
-        const int n2 = m * NWORDS / 2;
-        const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(gm);
-        ulonglong2* s2 = reinterpret_cast<ulonglong2*>(S.mask);
-        for (int base = threadIdx.x; base < n2; base += NT * 8) {
-            ulonglong2 v[8];
+        static_assert(NWORDS == 2 * (NT / 64), "two row blocks per wave");
+        const int nw = (m + 63) >> 6, wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        unsigned long long v[2][NWORDS];
+        int at[2][NWORDS];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = g2[min(base + NT * u, n2 - 1)];
+        for (int h = 0; h < 2; ++h) {
+            const int rb = h == 0 ? wv : NWORDS - 1 - wv;  // wave-uniform
+            const int i0 = 64 * rb, wn = nw - rb, cnt = rb < nw ? min(64, m - i0) * wn : 0;
+            const float inv = 1.f / (float)(wn > 0 ? wn : 1);
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (base + NT * u < n2) s2[base + NT * u] = v[u];
+            for (int u = 0; u < NWORDS; ++u) {
+                const int f = ln + 64 * u;
+                at[h][u] = -1;
+                if (f < cnt) {
+                    // f / wn exactly: f < 1024 and wn <= 16 keep (f + 0.5) / wn at least 1/32 from an integer
+                    const int r = (int)(((float)f + 0.5f) * inv);
+                    at[h][u] = (i0 + r) * NWORDS + rb + (f - r * wn);
+                    v[h][u] = gm[at[h][u]];
+                }
+            }
         }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int u = 0; u < NWORDS; ++u)
+                if (at[h][u] >= 0) S.mask[at[h][u]] = v[h][u];
     }
     for (int t = threadIdx.x; t < m; t += NT) S.valid[t] = X.valid[(int64_t)seg * KC + t];
     __syncthreads();

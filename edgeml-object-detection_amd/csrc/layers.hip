@@ -75,54 +75,6 @@ __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int 
     return f32x4{v[0], v[1], v[2], 0.f};
 }
 
-#ifdef STEM_TABLE_DEBUG
-// Diagnostic build only: the round-4 uint8 table stem (c9d3a0e, withdrawn), rebuilt
-// with its LDS poisoned with NaN at entry and two end-of-kernel checks counted in g_stem_dbg: [0] table
-// entries that no longer equal their recomputed value (the table overwritten while the workgroup ran),
-// [1] LDS weight words that no longer equal the global weights, [2] non-finite stem outputs (a read of
-// a never-written LDS word).  edgedet_stem_debug_read copies the counters out.
-__device__ unsigned int g_stem_dbg[4];
-extern "C" int edgedet_stem_debug_read(unsigned int* out, int reset) {
-    EDGEDET_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stem_dbg), sizeof(unsigned int) * 4));
-    if (reset) {
-        const unsigned int z[4] = {0u, 0u, 0u, 0u};
-        EDGEDET_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stem_dbg), z, sizeof(z)));
-    }
-    return 0;
-}
-__device__ __forceinline__ f32x4 pre_pixel_lut(const uint8_t* __restrict__ xb, int H, int W, float sh, float sw,
-                                               const float* lut, int oy, int ox) {
-    float ry = sh * ((float)oy + 0.5f) - 0.5f;
-    float rx = sw * ((float)ox + 0.5f) - 0.5f;
-    ry = ry < 0.f ? 0.f : ry;
-    rx = rx < 0.f ? 0.f : rx;
-    const int y0 = (int)ry, x0 = (int)rx;
-    const int y1 = y0 + ((y0 < H - 1) ? 1 : 0);
-    const int x1 = x0 + ((x0 < W - 1) ? 1 : 0);
-    const float ly = ry - (float)y0, lx = rx - (float)x0;
-    const float hy = 1.f - ly, hx = 1.f - lx;
-    float v[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const uint8_t* src = xb + (int64_t)c * H * W;
-        const float* t = lut + 256 * c;
-#if STEM_TABLE_DEBUG > 1  // every byte load waited for (all counters) before its value indexes the table
-        const int i00 = src[(int64_t)y0 * W + x0], i01 = src[(int64_t)y0 * W + x1];
-        const int i10 = src[(int64_t)y1 * W + x0], i11 = src[(int64_t)y1 * W + x1];
-        __builtin_amdgcn_s_waitcnt(0);
-        const float a00 = t[i00], a01 = t[i01], a10 = t[i10], a11 = t[i11];
-#else
-        const float a00 = t[src[(int64_t)y0 * W + x0]];
-        const float a01 = t[src[(int64_t)y0 * W + x1]];
-        const float a10 = t[src[(int64_t)y1 * W + x0]];
-        const float a11 = t[src[(int64_t)y1 * W + x1]];
-#endif
-        v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
-    }
-    return f32x4{v[0], v[1], v[2], 0.f};
-}
-#endif
-
 // Host: may the uint8 transform use div_fast?  Every operand a uint8 image can give either division
 // (x = 0..255; then (x / 255 - mean_c) for each channel) is checked against the IEEE division; rstd
 // receives RN(1 / std_c).  (Host float arithmetic is IEEE single with -ffp-contract=off, fmaf exact.)
@@ -273,9 +225,6 @@ __global__ void __launch_bounds__(256) dwconv_se_kernel(DwParams p) {
 // per output drops by ~K/(1+(K-1)/PW).  Accumulation order per output is (kh, kw) as in the
 // scalar kernel.  SE variant: grid (cdiv(C/4,16), SE_PARTS, B), block = 16 quads x 16 group lanes,
 // partial sums per pixel-group split (see dwconv_se_kernel).
-#ifndef DW_PIPE
-#define DW_PIPE 0
-#endif
 template <int K, int S, int PW>
 __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restrict__ xb, int oh, int ow0, int c,
                                          f32x4 (&acc)[PW]) {
@@ -283,39 +232,6 @@ __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restr
 #pragma unroll
     for (int o = 0; o < PW; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int ih0 = oh * S - p.pad, iw0 = ow0 * S - p.pad;
-#if DW_PIPE
-    // every input row's loads issued before the first row's FMAs (clamped addresses, unconditional
-    // loads, out-of-image columns zeroed after the load; rows outside the image skipped as below, so
-    // the FMA sequence and its bits are unchanged)
-    f32x4 xin[K][IW];
-#pragma unroll
-    for (int kh = 0; kh < K; ++kh) {
-        const int ih = min(max(ih0 + kh, 0), p.H - 1);
-        const float* row = xb + (int64_t)ih * p.W * p.C;
-#pragma unroll
-        for (int j = 0; j < IW; ++j) {
-            const int iw = iw0 + j;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(row + (int64_t)min(max(iw, 0), p.W - 1) * p.C);
-            xin[kh][j] = (unsigned)iw < (unsigned)p.W ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    }
-#pragma unroll
-    for (int kh = 0; kh < K; ++kh) {
-        if ((unsigned)(ih0 + kh) >= (unsigned)p.H) continue;
-#pragma unroll
-        for (int kw = 0; kw < K; ++kw) {
-            const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (kh * K + kw) * p.C + c);
-#pragma unroll
-            for (int o = 0; o < PW; ++o) {
-                const f32x4 xv = xin[kh][o * S + kw];
-                acc[o].x = fmaf(xv.x, wv.x, acc[o].x);
-                acc[o].y = fmaf(xv.y, wv.y, acc[o].y);
-                acc[o].z = fmaf(xv.z, wv.z, acc[o].z);
-                acc[o].w = fmaf(xv.w, wv.w, acc[o].w);
-            }
-        }
-    }
-#else
 #pragma unroll
     for (int kh = 0; kh < K; ++kh) {
         const int ih = ih0 + kh;
@@ -341,7 +257,6 @@ __device__ __forceinline__ void dw_group(const DwParams& p, const float* __restr
             }
         }
     }
-#endif
 }
 
 template <int K, int S, int PW>
@@ -478,28 +393,6 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
     __shared__ __attribute__((aligned(16))) float ss[STEM_SH * STEM_SH * STEM_SS];
     __shared__ __attribute__((aligned(16))) float ws[STEM_NW];
     const int tid = threadIdx.x, b = blockIdx.y;
-#ifdef STEM_LDS_PAD  // diagnostic: the table variant's LDS footprint (54,992 B, 2 workgroups per CU) without a table
-    __shared__ float lds_pad[sizeof(T) == 1 && FUSED ? 3 * 256 : 1];
-    if (sizeof(T) == 1 && FUSED) {
-        for (int e = tid; e < 3 * 256; e += 256) lds_pad[e] = (float)e;
-        __syncthreads();
-        if (lds_pad[(tid * 7) % 768] < 0.f) return;  // never taken; keeps the array
-    }
-#endif
-#ifdef STEM_TABLE_DEBUG
-    constexpr bool TBL = sizeof(T) == 1 && FUSED;
-    __shared__ float lut[TBL ? 3 * 256 : 1];
-    if constexpr (TBL) {
-        const float qnan = __builtin_nanf("");
-        for (int e = tid; e < STEM_XH * STEM_XH * 4; e += 256) xs[e] = qnan;
-        for (int e = tid; e < STEM_SH * STEM_SH * STEM_SS; e += 256) ss[e] = qnan;
-        for (int e = tid; e < STEM_NW; e += 256) ws[e] = qnan;
-        for (int e = tid; e < 3 * 256; e += 256) lut[e] = qnan;
-        __syncthreads();
-        for (int e = tid; e < 3 * 256; e += 256) lut[e] = ((float)(e & 255) / 255.f - p.mean[e >> 8]) / p.stdv[e >> 8];
-        __syncthreads();
-    }
-#endif
     const int oh0 = (blockIdx.x / tiles_w) * STEM_T, ow0 = (blockIdx.x % tiles_w) * STEM_T;
     const int sh0 = oh0 - 1, sw0 = ow0 - 1;          // stem-output halo origin
     const int xh0 = 2 * sh0 - 1, xw0 = 2 * sw0 - 1;  // input tile origin (stem pad 1, stride 2)
@@ -527,12 +420,6 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             if constexpr (FUSED) {
                 const T* img = (const T*)(sizeof(T) == 1 ? (const void*)p.src8 : (const void*)p.src) +
                                (int64_t)b * 3 * p.H0 * p.W0;
-#ifdef STEM_TABLE_DEBUG
-                if constexpr (TBL)
-                    xv[r] = in ? pre_pixel_lut(p.src8 + (int64_t)b * 3 * p.H0 * p.W0, p.H0, p.W0, p.sh, p.sw, lut, ih, iw)
-                               : f32x4{0.f, 0.f, 0.f, 0.f};
-                else
-#endif
                 xv[r] = in ? pre_pixel<T, FAST>(img, p.H0, p.W0, p.sh, p.sw, p.mean, p.stdv, p.rstd, ih, iw)
                            : f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
@@ -619,29 +506,9 @@ __global__ void __launch_bounds__(256) ssd_stem_kernel(StemParams p, int tiles_w
             if (yh < p.Ho && yw < p.Wo) {
                 const float r = ss[((ph + 1) * STEM_SH + pw + 1) * STEM_SS + l16];
                 p.y[(((int64_t)b * p.Ho + yh) * p.Wo + yw) * 16 + l16] = (acc[i] + b1v) + r;
-#ifdef STEM_TABLE_DEBUG
-                if (TBL && !__builtin_isfinite((acc[i] + b1v) + r)) atomicAdd(&g_stem_dbg[2], 1u);
-#endif
             }
         }
     }
-#ifdef STEM_TABLE_DEBUG
-    if constexpr (TBL) {  // the table and the LDS weights still hold what was written at the start
-        for (int e = tid; e < 3 * 256; e += 256) {
-            const float v = ((float)(e & 255) / 255.f - p.mean[e >> 8]) / p.stdv[e >> 8];
-            if (__float_as_uint(v) != __float_as_uint(lut[e])) atomicAdd(&g_stem_dbg[0], 1u);
-        }
-        for (int e = tid; e < STEM_NW; e += 256) {
-            const float* src = e < STEM_B0   ? p.w0 + (e / 36) * p.ld0 + e % 36
-                               : e < STEM_WD ? p.b0 + (e - STEM_B0)
-                               : e < STEM_BD ? p.wd + (e - STEM_WD)
-                               : e < STEM_W1 ? p.bd + (e - STEM_BD)
-                               : e < STEM_B1 ? p.w1 + ((e - STEM_W1) / 16) * p.ld1 + (e - STEM_W1) % 16
-                                             : p.b1 + (e - STEM_B1);
-            if (__float_as_uint(*src) != __float_as_uint(ws[e])) atomicAdd(&g_stem_dbg[1], 1u);
-        }
-    }
-#endif
 }
 
 int ssd_stem_launch(const StemParams& p0, hipStream_t s) {

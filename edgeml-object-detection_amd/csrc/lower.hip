@@ -106,14 +106,16 @@ static uint16_t bf16_rn(float x, float* back) {
     return (uint16_t)r;
 }
 
-// plan.split_bf16x3: x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1); planes [3][n].
-static std::vector<uint16_t> split_bf16x3(const std::vector<float>& w) {
+// plan.split_bf16x3: x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1); planes [3][n] of rows of
+// kpad, x = -w in the odd 32-wide K blocks (the bf16x6 kernels' sign-alternated stages).
+static std::vector<uint16_t> split_bf16x3(const std::vector<float>& w, int64_t kpad) {
     const size_t n = w.size();
     std::vector<uint16_t> out(3 * n);
     for (size_t i = 0; i < n; ++i) {
         float f0, f1, f2;
-        out[i] = bf16_rn(w[i], &f0);
-        const float r1 = w[i] - f0;
+        const float x = (((int64_t)i % kpad) >> 5) & 1 ? -w[i] : w[i];
+        out[i] = bf16_rn(x, &f0);
+        const float r1 = x - f0;
         out[n + i] = bf16_rn(r1, &f1);
         const float r2 = r1 - f1;
         out[2 * n + i] = bf16_rn(r2, &f2);
@@ -248,7 +250,7 @@ class Packer {
         ConvW r;
         r.w = pk_.add(pk_.values ? wp.data() : nullptr, cout * Kpad);
         if (pk_.values) {
-            auto s = split_bf16x3(wp);
+            auto s = split_bf16x3(wp, Kpad);
             r.w.split = pk_.add_u16(s.data(), (int64_t)s.size()).off;
         } else {
             r.w.split = pk_.add_u16(nullptr, 3 * cout * Kpad).off;
@@ -928,9 +930,9 @@ class SSDLite {
             P.add(o);
         }
         const int64_t NS = NC - 1, KM = TOPK;
-        // EDGEDET_SSD_NMS=class: per-(image, class) NMS on every class's top-k, then the per-image merge
-        // (the form the image-greedy kernel replaced; an A/B switch)
-        if (NS * KM <= 512 * 54 && DETS <= 1024 && !env_is("EDGEDET_SSD_NMS", "class", "image")) {
+        // shapes past the image-greedy kernel's limits: per-(image, class) NMS on every class's top-k,
+        // then the per-image merge
+        if (NS * KM <= 512 * 54 && DETS <= 1024) {
             const int pk = P.buf({B, NS, KM}, I32, "pool.key" + sfx);
             const int pr = P.buf({B, NS, KM}, I32, "pool.ref" + sfx);
             OpRec o;
@@ -938,7 +940,7 @@ class SSDLite {
             o.name = "postprocess.nms" + sfx;
             const int64_t iv[5] = {B, A, NC, KM, DETS};
             for (int j = 0; j < 5; ++j) o.i[j] = iv[j];
-            o.i[5] = env_int("EDGEDET_SSD_SELECT_WAVE", 0);
+            o.i[5] = 0;  // class selection: the four-wave block form (1: the one-wave form, unit tests)
             o.p[0] = view(sh.scores_t);
             o.p[1] = view(sh.boxes);
             o.p[2] = P.ref(pk);
@@ -1770,7 +1772,7 @@ struct Engine {
     std::unique_ptr<SSDLite> ssd;
     std::unique_ptr<FasterRCNN> frcnn;
     std::unique_ptr<RetinaNet> retina;
-    std::map<std::tuple<int, int, int, bool>, std::unique_ptr<Plan>> plans;
+    std::map<std::tuple<int, int, int, bool, int64_t>, std::unique_ptr<Plan>> plans;  // (B, H, W, u8, redzone)
     uint64_t clock = 0;
 };
 constexpr size_t PLAN_CACHE = 64;
@@ -1805,7 +1807,7 @@ static Engine* engine(const Config& c) {
 }
 
 static Plan* plan_for(Engine* e, int B, int H, int W, bool u8) {
-    auto key = std::make_tuple(B, H, W, u8);
+    auto key = std::make_tuple(B, H, W, u8, g_redzone);  // a redzone layout never serves a plain lowering
     auto it = e->plans.find(key);
     if (it != e->plans.end()) {
         it->second->last_use = ++e->clock;
@@ -1892,8 +1894,7 @@ static int shape_ok(int32_t B, int32_t H, int32_t W) {
 extern "C" int edgedet_set_redzone(int64_t bytes) {
     EDGEDET_REQUIRE(bytes >= 0 && bytes % 256 == 0 && bytes <= (64 << 20), "set_redzone: 0..64 MiB, multiple of 256");
     std::lock_guard<std::mutex> g(g_mu);
-    g_redzone = bytes;
-    for (auto& kv : g_engines) kv.second->plans.clear();  // every later lowering lays out with the new gaps
+    g_redzone = bytes;  // part of the plan cache key: every later lookup lowers (or finds) the new layout
     return 0;
 }
 
@@ -2064,7 +2065,7 @@ extern "C" int edgedet_model_release(int32_t kind, int32_t num_classes, int32_t 
     if (config_of(kind, num_classes, reduced_tail, &c) || shape_ok(B, H, W)) return -1;
     EDGEDET_TRY({
         std::lock_guard<std::mutex> g(g_mu);
-        engine(c)->plans.erase(std::make_tuple(B, H, W, input_u8 != 0));
+        engine(c)->plans.erase(std::make_tuple(B, H, W, input_u8 != 0, g_redzone));
         return 0;
     })
 }

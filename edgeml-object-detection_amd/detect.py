@@ -7,7 +7,10 @@ Behaviour kept from the reference (detect.py:62-106): images are taken in sorted
 read as RGB and scaled by 1/255, every image gets one ``<name[:-4]>.npy`` (N,6) float64 file
 ``[cls, xc, yc, w, h, conf]`` normalised by the original size, rows in score order, an empty result
 still writes a (0,6) file.  Differences: images of equal size are batched across the whole list
-(results are per image and identical to batch=1) and decoded ahead of the engine (baseline JPEGs:
+(results are per image, but their last bits depend on the batch an image runs in: conv tiles are
+chosen per batch size, so a different summation order can move a score by float32 rounding; the
+grouping is a fixed function of the sorted list, so a given list always gives the same files) and
+decoded ahead of the engine (baseline JPEGs:
 Huffman decoding on a host thread pool, IDCT / upsampling / colour conversion on the GPU, csrc/jpeg.hip,
 byte-identical to the host decoder; other files on the host),
 and under ``torchrun`` the single-process run's batch list is split into contiguous blocks of

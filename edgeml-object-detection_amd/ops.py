@@ -119,7 +119,7 @@ def lib():
                                     _vp, _vp, _i32, _vp]
     L.edgedet_conv2d_x3.argtypes = [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
                                     _i32, _vp, _vp, _i32, _vp]
-    L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _vp, _vp]
+    L.edgedet_split_bf16x3.argtypes = [_vp, _i64, _i64, _vp, _vp]
     L.edgedet_mlp_state_size.argtypes = [_i32, _vp]
     L.edgedet_mlp_state_size.restype = ctypes.c_int64
     L.edgedet_mlp_fit.argtypes = [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -254,11 +254,12 @@ def roi_align_nhwc(feat_nhwc, rois, spatial_scale, output_size=7, sampling_ratio
 
 
 def split_bf16x3(w):
-    """Device split of an fp32 tensor into three bf16 planes (uint16 bit patterns, [3, *w.shape]):
-    the weights of the bf16x6 conv tiles (edgedet_split_bf16x3; same split as plan.split_bf16x3)."""
+    """Device split of packed fp32 weights [Cout, Kpad] into three bf16 planes (uint16 bit patterns,
+    [3, Cout, Kpad], the odd 32-wide K blocks of -w): the weights of the bf16x6 conv tiles
+    (edgedet_split_bf16x3; same split as plan.split_bf16x3)."""
     _need_cuda(w)
     out = torch.empty((3,) + tuple(w.shape), dtype=torch.int16, device=w.device)
-    check(lib().edgedet_split_bf16x3(_ptr(w), w.numel(), _ptr(out), stream_handle()))
+    check(lib().edgedet_split_bf16x3(_ptr(w), w.numel(), w.shape[-1], _ptr(out), stream_handle()))
     return out
 
 

@@ -61,9 +61,13 @@ def _bf16_rn(x):
 
 
 def split_bf16x3(w):
-    """fp32 w -> uint16 [3, *w.shape]: x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1) (= exact).
-    The weight operand of the bf16x6 conv tiles (same arithmetic as csrc/conv.hip split3_bf16)."""
+    """fp32 packed weights w [Cout, Kpad] -> uint16 [3, Cout, Kpad]: x0 = RN(x), x1 = RN(x - x0),
+    x2 = RN(x - x0 - x1) (= exact) of x = w, and of x = -w in the odd 32-wide K blocks (k // 32 odd):
+    the weight operand of the bf16x6 conv tiles, whose sign-alternated stages subtract those blocks'
+    sums (csrc/conv.hip conv_x6b_body; the same arithmetic as split_bf16x3_kernel)."""
     w = np.ascontiguousarray(w, dtype=np.float32)
+    assert w.shape[-1] % 32 == 0, "rows of Kpad, a multiple of 32"
+    w = np.where((np.arange(w.shape[-1]) // 32) % 2 == 1, -w, w).astype(np.float32)
     h0, f0 = _bf16_rn(w)
     r1 = (w - f0).astype(np.float32)
     h1, f1 = _bf16_rn(r1)

@@ -106,9 +106,11 @@ int edgedet_graph_launch(void* graph, void* stream);
 int edgedet_graph_destroy(void* graph);
 
 /* Diagnostic: leave `bytes` (a multiple of 256, 0 = none, the default) unused before, between and after
- * the workspace buffers of every plan lowered from now on (cached lowerings are dropped), so a caller
- * can fill the gaps with a canary and catch a kernel writing outside its buffers
- * (tests/test_gpu_redzone.py). */
+ * the workspace buffers of every plan looked up from now on (the redzone is part of the plan cache key,
+ * so layouts with and without gaps never mix), so a caller can fill the gaps with a canary and catch a
+ * kernel writing outside its buffers (tests/test_gpu_redzone.py).  The layout changes with the
+ * setting: query edgedet_model_workspace_size and run edgedet_model_prepare again after every call
+ * before the next forward -- a workspace sized before the switch is too small for the new layout. */
 int edgedet_set_redzone(int64_t bytes);
 
 /* ------------------------------------------------------------------------ model forward */
@@ -279,8 +281,11 @@ int edgedet_conv2d_x3(const float* x, uint16_t* x3, int64_t B, int64_t H, int64_
                       const float* w, const uint16_t* w3, const float* bias, int64_t Cout, int32_t KH,
                       int32_t KW, int32_t stride, int32_t pad, int32_t act, const float* res, float* y,
                       int32_t tile, void* stream);
-/* w [n] fp32 -> out [3][n] bf16 bit patterns: x0 = RN(x), x1 = RN(x - x0), x2 = x - x0 - x1 (exact). */
-int edgedet_split_bf16x3(const float* w, int64_t n, uint16_t* out, void* stream);
+/* Packed weights w [n / kpad][kpad] fp32 -> out [3][n] bf16 bit patterns: x0 = RN(x), x1 = RN(x - x0),
+ * x2 = x - x0 - x1 (exact), of x = w, and of x = -w in the odd 32-wide K blocks (k / 32 odd): the
+ * bf16x6 kernels subtract those stages' sums, which cancels the matrix cores' truncation bias
+ * (csrc/conv.hip conv_x6b_body).  kpad: a multiple of 32 dividing n. */
+int edgedet_split_bf16x3(const float* w, int64_t n, int64_t kpad, uint16_t* out, void* stream);
 
 /*
  * SSDLite stem + first block in one pass: y = proj(relu(dw3x3(s))) + b1 + s with

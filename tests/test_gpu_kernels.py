@@ -343,8 +343,8 @@ def test_split_bf16x3_device_matches_host():
     from edgeml_amd import ops
     from edgeml_amd.plan import split_bf16x3
     g = torch.Generator().manual_seed(3)
-    w = torch.cat([torch.randn(40000, generator=g) * 10 ** torch.randint(-6, 4, (40000,), generator=g),
-                   torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0e38, 1e-38, 65504.0])])
+    w = torch.cat([torch.randn(40025, generator=g) * 10 ** torch.randint(-6, 4, (40025,), generator=g),
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0e38, 1e-38, 65504.0])]).reshape(139, 288)  # Kpad 288
     got = ops.split_bf16x3(w.to(DEV)).cpu().numpy().view(np.uint16)
     assert np.array_equal(got, split_bf16x3(w.numpy()))
 

@@ -81,17 +81,23 @@ def test_group_launch_equals_members_one_by_one(which):
     assert kinds == ({ops.CONV, ops.DWCONV} if which == 0 else {ops.CONV}), (name, kinds)
 
 
+@pytest.mark.parametrize("size", [(640, 640), (427, 640)])
 @pytest.mark.parametrize("pattern", ["quantized", "all_equal", "continuous", "two_values"])
-def test_rpn_chunked_split_equal_single_pass(pattern):
+def test_rpn_chunked_split_equal_single_pass(pattern, size):
+    """The four RPN selection forms write the same records.  640 x 640 (resized 800 x 800): P2's 15
+    chunks take the split selection's register bisection; 427 x 640 (a COCO size, resized 800 x 1199,
+    padded 800 x 1216): P2's 23 chunks exceed its 16 and take the radix select + compact fallback."""
     B = 2
     m = models.FasterRCNNFPNv2(synthetic.synthetic_state_dict("faster_rcnn", 91), 91).to("cuda")
-    plan = m.plan(B, 640, 640)
+    plan = m.plan(B, *size)
     k = next(j for j, op in enumerate(plan.ops) if op.kind == ops.RPN_LEVEL_NMS)
     rec = plan.records[k:k + 1].copy()
     rec["i"][0, ops.LANE_FIELD] = 0
     L, KM = int(rec["i"][0, 1]), int(rec["i"][0, 5])
     ns = [int(rec["i"][0, 6 + l]) for l in range(L)]
     assert max(ns) > 8192 * 4 and min(ns) < 1000, ns  # several chunks at P2, n < topk at P6
+    nch = (max(ns) + 8191) // 8192
+    assert (nch <= 16) == (size == (640, 640)), (ns, nch)  # the register path's limit: 16 chunks
     assert rec["p"][0, 20] and rec["i"][0, 16] == 8192
     g = torch.Generator().manual_seed(hash(pattern) % 1000)
     for l, n in enumerate(ns):

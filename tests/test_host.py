@@ -213,15 +213,18 @@ def test_frcnn_plan_lowering():
 
 
 def test_split_bf16x3_is_exact():
-    """The three bf16 planes of plan.split_bf16x3 sum back to the fp32 value exactly, each term is a
-    bf16 bit pattern, and the terms shrink by >= 2^8 (RN split: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|)."""
+    """The three bf16 planes of plan.split_bf16x3 sum back to the fp32 value exactly (negated in the
+    odd 32-wide K blocks: the bf16x6 kernels' sign-alternated stages), each term is a bf16 bit pattern,
+    and the terms shrink by >= 2^8 (RN split: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|)."""
     import numpy as np
     from edgeml_amd.plan import split_bf16x3
     rng = np.random.default_rng(0)
-    w = (rng.standard_normal(100000) * 10.0 ** rng.integers(-8, 8, 100000)).astype(np.float32)
+    w = (rng.standard_normal(100000) * 10.0 ** rng.integers(-8, 8, 100000)).astype(np.float32).reshape(625, 160)
     planes = split_bf16x3(w)
     vals = (planes.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
-    assert np.array_equal(vals.sum(0), w.astype(np.float64))
+    sign = np.where((np.arange(160) // 32) % 2 == 1, -1.0, 1.0)
+    assert np.array_equal(vals.sum(0), w.astype(np.float64) * sign)
+    assert np.array_equal(vals.sum(0)[:, :32], w[:, :32].astype(np.float64))
     a = np.abs(w.astype(np.float64))
     assert np.all(np.abs(vals[1]) <= a * 2.0 ** -8 * (1 + 1e-7))
     assert np.all(np.abs(vals[2]) <= a * 2.0 ** -16 * (1 + 1e-7))

@@ -2,9 +2,10 @@
 
     python tools/accuracy_probe.py
 
-1. Error of one FRCNN-shaped conv (3x3 256 -> 256, K = 2304; 1x1 1024 -> 256; 1x1 2048 -> 512) against
-   a float64 conv: the bf16x6 tiles (39, 25, 38), the exact-fp32 MFMA tile (3) and torch's CPU fp32
-   conv (the oracle's arithmetic).  Max and RMS error relative to max |y|.
+1. Error of one FRCNN-shaped conv (3x3 256 -> 256, K = 2304; 1x1 1024 -> 256; 1x1 2048 -> 512; the box
+   head's fc6, 1x1 12544 -> 1024 over 1,000 RoIs) against a float64 conv: the bf16x6 tiles, the fp32
+   MFMA kernels, the plain fmaf-chain tile (3) and torch's CPU fp32 conv (the oracle's arithmetic).
+   Max and RMS error and mean (bias) relative to max |y|.
 2. The matrix cores' accumulation: a 1x1 conv whose one output sums 1.0 and 31 (or 63) copies of
    t = 2^-25 (every term exact in bf16 and its products exact): the exact sum is 1 + 31 t =
    1 + 7.75 ulp(1).  Round-to-nearest of the exact sum gives 1 + 8 ulp, truncation 1 + 7, and a
@@ -25,8 +26,13 @@ def conv_errors():
     from edgeml_amd import ops
     from edgeml_amd.plan import pack_conv_weight
     dev = "cuda"
-    for (B, H, W, Cin, Cout, k, tiles) in ((1, 100, 100, 256, 256, 3, (39, 25, 3)), (1, 50, 50, 1024, 256, 1, (39, 25, 3)),
-                                           (1, 25, 25, 2048, 512, 1, (39, 25, 3)), (2, 56, 56, 64, 64, 3, (38, 3))):
+    # tiles: 39 / 25 / 29 / 31 / 38 / 21 the bf16x6 kernels (stage sums since round 6), 3 the exact-fp32
+    # MFMA tile with the plain fmaf chain (the accuracy reference), 5 / 14 / 16 the fp32 MFMA kernels
+    # with stage sums; the last case is the FRCNN box head's fc6 at 1,000 RoIs (K = 12,544)
+    for (B, H, W, Cin, Cout, k, tiles) in ((1, 100, 100, 256, 256, 3, (39, 25, 29, 31, 21, 3, 5)),
+                                           (1, 50, 50, 1024, 256, 1, (39, 25, 3, 16)),
+                                           (1, 25, 25, 2048, 512, 1, (39, 25, 3, 16)), (2, 56, 56, 64, 64, 3, (38, 3)),
+                                           (1000, 1, 1, 12544, 1024, 1, (25, 14, 3))):
         g = torch.Generator().manual_seed(3)
         # post-ReLU activations (non-negative) and zero-mean weights, as in the ResNet body
         x = torch.relu(torch.randn(B, Cin, H, W, generator=g))
@@ -42,7 +48,7 @@ def conv_errors():
         w3 = ops.split_bf16x3(wp)
         for t in tiles:
             y = ops.conv2d_nhwc(xd, wp, b.to(dev), Cout, k, 1, (k - 1) // 2, None, tile=t,
-                                w3=None if t == 3 else w3)
+                                w3=w3 if t >= 21 else None)
             res[f"tile{t}"] = y.permute(0, 3, 1, 2).double().cpu() - ref
         line = " ".join(f"{n}: max {e.abs().max().item() / scale:.2e} rms {e.pow(2).mean().sqrt().item() / scale:.2e} "
                         f"bias {e.mean().item() / scale:+.1e}" for n, e in res.items())

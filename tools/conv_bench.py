@@ -4,6 +4,7 @@ import argparse
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -47,7 +48,8 @@ def main():
         x = torch.randn(B, H, W, Cin, device=dev)
         w = torch.randn(Cout, Cin, k, k) / (Cin * k * k) ** 0.5
         wp = torch.from_numpy(pack_conv_weight(w.numpy())[0]).to(dev)
-        w3 = ops.split_bf16x3(wp)
+        from edgeml_amd.plan import split_bf16x3
+        w3 = torch.from_numpy(split_bf16x3(wp.cpu().numpy()).view(np.int16)).to(dev)  # host split: any library
         b = torch.zeros(Cout, device=dev)
         Ho = (H + 2 * pad - k) // s + 1
         Wo = (W + 2 * pad - k) // s + 1

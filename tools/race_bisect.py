@@ -26,10 +26,8 @@ def main():
     ap.add_argument("--n", type=int, default=2, help="instances in flight at once")
     ap.add_argument("--ref-after", type=int, default=0, help="extra solo runs before the reference is taken")
     ap.add_argument("--detail", default="", help="buffer name prefix to describe when it differs (count, max |diff|, where)")
-    ap.add_argument("--stem-debug", action="store_true",
-                    help="a -DSTEM_TABLE_DEBUG build (EDGEDET_LIB): print its table-stem LDS check counters per trial")
     a = ap.parse_args()
-    from edgeml_amd import models, synthetic, ops
+    from edgeml_amd import models, synthetic
     if a.kind == "ssd":
         m = models.SSDLite320(synthetic.synthetic_state_dict("ssd", 91, True, seed=0), 91, True).to("cuda:0")
     else:
@@ -58,12 +56,6 @@ def main():
         torch.cuda.synchronize()
     ref = {b.name: b.tensor().clone() for b in bufs}
     ref_host = {b.name: ref[b.name].cpu() for b in bufs}  # to tell a changed reference copy from a changed buffer
-    if a.stem_debug:
-        import ctypes
-        c = (ctypes.c_uint * 4)()
-        ops.check(ops.lib().edgedet_stem_debug_read(c, 1))
-        print(f"solo (capture + reference runs): stem LDS checks: table changed {c[0]}, weights changed {c[1]}, "
-              f"non-finite outputs {c[2]}", flush=True)
     for t in range(a.trials):
         for k in range(a.n):
             plans[k].input.tensor().copy_(imgs[k])
@@ -75,13 +67,7 @@ def main():
                 plans[k].replay(streams[k])
         torch.cuda.synchronize()
         bad = [b.name for b in bufs if not torch.equal(b.tensor(), ref[b.name])]
-        extra = ""
-        if a.stem_debug:
-            import ctypes
-            c = (ctypes.c_uint * 4)()
-            ops.check(ops.lib().edgedet_stem_debug_read(c, 1))
-            extra = f"; stem LDS checks: table changed {c[0]}, weights changed {c[1]}, non-finite outputs {c[2]}"
-        print(f"trial {t}: {len(bad)} of {len(bufs)} buffers differ; first: {bad[:6]}{extra}", flush=True)
+        print(f"trial {t}: {len(bad)} of {len(bufs)} buffers differ; first: {bad[:6]}", flush=True)
         moved = [n for n in ref if not torch.equal(ref[n].cpu(), ref_host[n])]
         if moved:
             print(f"  the device reference copies of {len(moved)} buffers changed since they were taken "
