@@ -865,15 +865,6 @@ constexpr int X3Z = 32;  // leading zero elements of a pre-split scratch (16-B a
 __device__ __forceinline__ int swz_key(int row) { return (row >> 2) & 2; }
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 32 + 8 * (chunk ^ swz_key(row)); }
 
-#ifndef X6_SLEEP
-#define X6_SLEEP 0
-#endif
-#ifndef X6_SB
-#define X6_SB 0
-#endif
-#ifndef X6_FRESH
-#define X6_FRESH 0
-#endif
 // XF: the input transform is active (SE scale / GN shift / ReLU); UT: Cin % 32 == 0, so every stage
 // lies inside one filter tap and the tap decomposition is wave-uniform (scalar) work.
 // PS: the input arrives pre-split (p.x3: three dense bf16 planes written by split_act_kernel, input
@@ -1207,13 +1198,14 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
             for (int pl = 0; pl < 3; ++pl) F.b[u][pl] = *reinterpret_cast<const bf16x8*>(Bb + pl * PB + o);
         }
     };
-    // quadrant (ha, hb) from the A half in FA and the B half in FB.  The stage's six split products
-    // (smallest first: a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0) chain into a fresh stage sum that
-    // starts at zero, and the running output takes that sum with ONE fp32 add (stage_add): each MFMA
-    // rounds its lane-group partial sums into C one group at a time, so chaining the six terms into
-    // the running output rounded it 24 times per stage at its full magnitude; the stage sum takes
-    // those roundings at the stage's (K/32 times smaller) magnitude.  RMS error against float64 on
-    // the 3x3 256->256 conv 1.39e-7 -> about 3e-8, below torch's CPU conv.
+    // Stage sums (mfma16 below: quadrant (ha, hb) from the A half in FA and the B half in FB).  The
+    // stage's six split products (smallest first: a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0) chain into
+    // a fresh stage sum that starts at zero, and the running output takes that sum with ONE fp32 add:
+    // each MFMA rounds its lane-group partial sums into C one group at a time, so chaining the six
+    // terms into the running output rounded it 24 times per stage at its full magnitude; the stage
+    // sum takes those roundings at the stage's (K/32 times smaller) magnitude.  RMS error against
+    // float64 on the 3x3 256->256 conv 1.39e-7 -> 3.2e-8, below torch's CPU conv.
+    // Cost: the adds are VALU work the old chain did not have (box head 3x3 2.08 -> 2.36 ms).
     // A tile's stage-sum add is issued after the NEXT tile's six MFMAs (pend), so the MFMA result it
     // reads has landed and no wait states separate them; flush() adds the last pending one.
     struct Pend {
@@ -1223,13 +1215,9 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
     } pend{f32x4{0.f, 0.f, 0.f, 0.f}, 1.f, -1, -1};
     auto flush = [&]() {
         if (pend.i >= 0) {
-#if X6_FRESH == 1
-            acc4[pend.i][pend.j] = pend.v;  // timing experiment only: no add (wrong results)
-#else
 #pragma unroll
             for (int r = 0; r < 4; ++r)  // c +- s, one rounding
                 acc4[pend.i][pend.j][r] = __builtin_fmaf(pend.sg, pend.v[r], acc4[pend.i][pend.j][r]);
-#endif
         }
         pend.i = -1;
     };
@@ -1238,21 +1226,17 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
         for (int t = 0; t < TM; ++t)
 #pragma unroll
             for (int u = 0; u < TN; ++u) {
-#if X6_FRESH == 2
-                f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][2], FB.b[u][0], acc4[ha * TM + t][hb * TN + u],
-                                                                  0, 0, 0);  // timing experiment: the old chain
-#else
                 f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][2], FB.b[u][0], f32x4{0.f, 0.f, 0.f, 0.f},
                                                                   0, 0, 0);
-#endif
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][1], FB.b[u][1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][2], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][1], FB.b[u][0], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA.a[t][0], FB.b[u][0], c, 0, 0, 0);
-#if X6_SB
-                __builtin_amdgcn_sched_barrier(X6_SB);  // the previous tile's add stays behind this chain
-#endif
+                // nothing but memory and scalar work crosses: the previous tile's add stays behind this
+                // chain (left free, the scheduler pulls each add up against its own chain and the two
+                // serialise on a wait for the MFMA result; box head 3x3 2.44 -> 2.36 ms)
+                __builtin_amdgcn_sched_barrier(0x3F4);
                 flush();
                 pend = Pend{c, sg, ha * TM + t, hb * TN + u};
             }
@@ -1283,9 +1267,6 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
             if (kc + 1 < nk) load_stage(r0, next_k(ca), buf ^ 1);
             read16(F0, buf, 0);
             __builtin_amdgcn_sched_barrier(0);  // issue the reads before the carried quadrant that hides them
-#if X6_SLEEP
-            if (wid >= 4) __builtin_amdgcn_s_sleep(X6_SLEEP);
-#endif
             mfma16(F1, F1, 1, 1, sgc);
             __builtin_amdgcn_sched_barrier(0);  // F1 is rewritten only after the carried quadrant issued
             sgc = buf ? sgb1 : sgb0;
@@ -1298,7 +1279,6 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
             // Spread the split VALU, the LDS writes of stage k+1 and the fragment reads over the gaps
             // of the MFMAs (1 MFMA : 1 LDS read : 3 VALU : 1 LDS write; 0 groups cost FRCNN 3%, 1..5
             // VALU within 1%) instead of letting them bunch up after the last MFMA.
-#ifndef X6_NOSGB
 #pragma unroll
             for (int i = 0; i < TM * TN * 18; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -1306,7 +1286,6 @@ __device__ __forceinline__ void conv_x6b_body(const ConvParams& p, const int blk
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
                 __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
             }
-#endif
             __syncthreads();
         }
         mfma16(F1, F1, 1, 1, sgc);

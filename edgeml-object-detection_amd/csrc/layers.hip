@@ -49,14 +49,18 @@ __device__ __forceinline__ float pre_load(const T* src, int64_t i) {
 template <typename T, bool FAST = false>
 __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int W, float sh, float sw,
                                            const float* mean, const float* stdv, const float* rstd, int oy, int ox) {
-    float ry = sh * ((float)oy + 0.5f) - 0.5f;
-    float rx = sw * ((float)ox + 0.5f) - 0.5f;
+    // ATen's CPU upsample_bilinear2d as built (contracted): src = fma(scale, dst + 0.5, -0.5), clamped
+    // at 0; index = min(floor(src), size - 1); lambda = clamp(src - index, 0, 1); each linear step
+    // fma(t0, lambda0, t1 * lambda1), width first (bit-identical to F.interpolate on the CPU oracle,
+    // tests/test_resize_rule.py)
+    float ry = __builtin_fmaf(sh, (float)oy + 0.5f, -0.5f);
+    float rx = __builtin_fmaf(sw, (float)ox + 0.5f, -0.5f);
     ry = ry < 0.f ? 0.f : ry;
     rx = rx < 0.f ? 0.f : rx;
-    const int y0 = (int)ry, x0 = (int)rx;
+    const int y0 = min((int)ry, H - 1), x0 = min((int)rx, W - 1);
     const int y1 = y0 + ((y0 < H - 1) ? 1 : 0);
     const int x1 = x0 + ((x0 < W - 1) ? 1 : 0);
-    const float ly = ry - (float)y0, lx = rx - (float)x0;
+    const float ly = fminf(fmaxf(ry - (float)y0, 0.f), 1.f), lx = fminf(fmaxf(rx - (float)x0, 0.f), 1.f);
     const float hy = 1.f - ly, hx = 1.f - lx;
     float v[3];
 #pragma unroll
@@ -70,7 +74,7 @@ __device__ __forceinline__ f32x4 pre_pixel(const T* __restrict__ xb, int H, int 
         const float a01 = norm((int64_t)y0 * W + x1);
         const float a10 = norm((int64_t)y1 * W + x0);
         const float a11 = norm((int64_t)y1 * W + x1);
-        v[c] = (a00 * hx + a01 * lx) * hy + (a10 * hx + a11 * lx) * ly;
+        v[c] = __builtin_fmaf(__builtin_fmaf(a00, hx, a01 * lx), hy, __builtin_fmaf(a10, hx, a11 * lx) * ly);
     }
     return f32x4{v[0], v[1], v[2], 0.f};
 }

@@ -134,6 +134,10 @@ def frcnn_check(plan, sd, num_classes, imgs, what="frcnn", own_check=2):
         tB = replay(sB, chains.RPN_STAGES)
         n = int(pc[b])
         assert len(tB.out) == n, (what, b, len(tB.out), n)  # decode + sigmoid recomputed on the host: 1-ulp tolerance
+        # (two proposals whose recomputed scores tie within an ulp may come out swapped: matched in
+        # the engine's order within a 16-place window, e2e_witness._engine_order)
+        from tests.e2e_witness import _engine_order
+        tB.out = _engine_order(sB, tB.out, props[b, :n])
         np.testing.assert_allclose(sB.box[tB.out], props[b, :n], rtol=2e-6, atol=1e-4)
         sA = chains.rpn_side([t[b] for t in objs], [t[b] for t in dels], anchors, sizes[b])
         tA = replay(sA, chains.RPN_STAGES)

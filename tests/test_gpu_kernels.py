@@ -227,7 +227,9 @@ def test_transform_u8_equals_float_image(H0, W0):
     """The transform record on the decoded uint8 image (each tap's divisions by div_fast on the device,
     bit-identical to the IEEE divisions on every uint8 operand: tests/test_fast_div.py) equals the
     transform of the host's float image / 255 (detect.py:58) bit for bit, with the FRCNN / RetinaNet
-    ImageNet normalisation (divisions that are not exact) and the SSD one."""
+    ImageNet normalisation (divisions that are not exact) and the SSD one; and both equal the CPU
+    oracle's GeneralizedRCNNTransform arithmetic (normalise, then F.interpolate bilinear on the CPU,
+    oracle/tv_ops.transform) bit for bit, up- and downscaling."""
     import ctypes
     from edgeml_amd import ops
     B = 2
@@ -250,6 +252,11 @@ def test_transform_u8_equals_float_image(H0, W0):
             outs.append(x4.cpu())
         assert torch.isfinite(outs[0]).all()
         assert torch.equal(outs[0], outs[1]), (norm, int((outs[0] != outs[1]).sum()))
+        m = torch.tensor(norm[:3])[:, None, None]
+        sd = torch.tensor(norm[3:])[:, None, None]
+        ref = F.interpolate((img8.float() / 255 - m) / sd, size=(Ho, Wo), mode="bilinear", align_corners=False)
+        got = outs[1][..., :3].permute(0, 3, 1, 2)
+        assert torch.equal(got, ref), (norm, int((got != ref).sum()), float((got - ref).abs().max()))
 
 
 @pytest.mark.parametrize("B,C,S,parts", [(1, 72, 24, 16), (32, 960, 240, 1), (7, 120, 32, 5), (64, 672, 168, 2),

@@ -70,12 +70,10 @@ def test_engine_orie_no_further_from_f64_than_the_f32_oracle():
     de, do = np.abs(o["eng"] - o["f64"]), np.abs(o["f32"] - o["f64"])
     print(f"|ORIE - ORIE_f64|: engine max {de.max():.3e} mean {de.mean():.3e} ({np.count_nonzero(de)} images); "
           f"f32 oracle max {do.max():.3e} mean {do.mean():.3e} ({np.count_nonzero(do)} images)")
+    # the worst case, the typical and the count, with no slack: since round 6 the
+    # conv kernels accumulate per-stage sums with sign-alternated K blocks (csrc/conv.hip conv_x6b_body,
+    # tools/accuracy_probe.py: RMS 3.2e-8 against the CPU conv's 3.4e-8, bias 4e-11), so the engine's
+    # detections are no further from the float64 truth than the float32 CPU oracle's on every measure
     assert de.max() <= do.max(), (de.max(), do.max())
-    # the typical and the count as well as the worst case: the engine's matrix cores
-    # truncate each bf16 product to the ulp of the largest of its 8-product group (tools/mfma_probe.py,
-    # profiles/r5d_mfma_probe.txt), so its conv outputs carry ~4x the RMS error of the CPU's fp32
-    # convs (tools/accuracy_probe.py); ORIE differences come from the detections those errors move
-    # (every one attributed by tests/test_gpu_frcnn_e2e.py), so the engine may differ from the
-    # float64 truth on a few more images than the float32 oracle, never by more in the worst case
-    assert de.mean() <= 1.5 * do.mean() + 1e-6, (de.mean(), do.mean())
-    assert np.count_nonzero(de) <= np.count_nonzero(do) + 2, (np.count_nonzero(de), np.count_nonzero(do))
+    assert de.mean() <= do.mean(), (de.mean(), do.mean())
+    assert np.count_nonzero(de) <= np.count_nonzero(do), (np.count_nonzero(de), np.count_nonzero(do))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Accuracy session: the conv accuracy probe, the FRCNN stage-error table, then (TESTS=1) the GPU
+# Accuracy session: the conv accuracy probe, the FRCNN stage- and layer-error tables, then (TESTS=1) the GPU
 # parity tests and (BENCH=1) the bench at the driver's arguments.  Stops on a fault or time limit.
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
@@ -18,6 +18,7 @@ step() {
 }
 step accuracy 300 python -u tools/accuracy_probe.py
 step stage_error 600 python -u tools/stage_error.py --images 0,1,2 -o gpurun_out/stage_error.json
+step layer_error 600 python -u tools/layer_error.py --image 0
 if [ "${TESTS:-1}" = "1" ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
 fi
