@@ -30,7 +30,10 @@ if [ "${STAGE:-1}" = "1" ]; then
   step stage_error 600 python -u tools/stage_error.py --images 0,1,2 -o gpurun_out/stage_error.json
 fi
 if [ "${PROF:-1}" = "1" ]; then
-  step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o trace -- python3 bench.py --model both --no-cpu --no-e2e --steps 200
+  step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_trace -o trace -- python3 bench.py --model both --no-cpu --no-e2e --steps 200
+  # the raw trace stays on the box (tens of MB): its per-kernel stats and the stretch attribution come back
+  find /tmp/prof_trace -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \;
+  python3 tools/stretch.py /tmp/prof_trace --kernel conv_x6b_group_kernel -o gpurun_out/stretch.txt >> gpurun_out/steps.log 2>&1
   for m in ssd frcnn; do
     step bench_fetch_$m 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$m -o fetch -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu --no-e2e
     step bench_write_$m 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$m -o write -- python3 bench.py --model $m --steps 2 --warmup 1 --no-cpu --no-e2e
