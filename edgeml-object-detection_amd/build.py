@@ -17,6 +17,10 @@ LIB = os.path.join(HERE, "libedgedet.so")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# Per-file flags.  conv.hip: no SLP vectorisation, so the stage-sum adds and the operand split stay
+# scalar v_fmac_f32 / v_sub_f32: beside MFMAs a packed f32 op costs about three scalar ones
+# (MI355X_MICROARCH.md, 'price of one filler beside MFMAs').
+FILE_FLAGS = {"conv.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc():
@@ -61,11 +65,12 @@ def up_to_date():
 DIAG_LIB = os.path.join(HERE, "libedgedet_diag.so")
 
 
-def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=()):
+def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=(), extra_flags=()):
     """diag=True: libedgedet_diag.so with -DEDGEDET_DIAG (the EDGEDET_DIAG_SKIP op-family skips of
     csrc/exec.hip, wrong results; load it with EDGEDET_LIB, tools/gpu_skip.sh).  variant="name" with
     defines=("NMS_PROFILE", ...): libedgedet_<name>.so built with those -D flags (diagnostic builds,
-    loaded with EDGEDET_LIB).  Never the product."""
+    loaded with EDGEDET_LIB); extra_flags: further hipcc flags of such a variant (A/B builds).  Never
+    the product."""
     if variant:
         diag = True
     lib = os.path.join(HERE, f"libedgedet_{variant}.so") if variant else (DIAG_LIB if diag else LIB)
@@ -78,8 +83,8 @@ def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")
-        dflags = [f"-D{d}" for d in defines] if variant else (["-DEDGEDET_DIAG"] if diag else [])
-        cmd = [cc, *FLAGS, *dflags, "-I", objdir, "-c", src, "-o", obj]
+        dflags = [f"-D{d}" for d in defines] + list(extra_flags) if variant else (["-DEDGEDET_DIAG"] if diag else [])
+        cmd = [cc, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *dflags, "-I", objdir, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
