@@ -65,12 +65,13 @@ def up_to_date():
 DIAG_LIB = os.path.join(HERE, "libedgedet_diag.so")
 
 
-def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=(), extra_flags=()):
+def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=(), extra_flags=(), only=()):
     """diag=True: libedgedet_diag.so with -DEDGEDET_DIAG (the EDGEDET_DIAG_SKIP op-family skips of
     csrc/exec.hip, wrong results; load it with EDGEDET_LIB, tools/gpu_skip.sh).  variant="name" with
     defines=("NMS_PROFILE", ...): libedgedet_<name>.so built with those -D flags (diagnostic builds,
-    loaded with EDGEDET_LIB); extra_flags: further hipcc flags of such a variant (A/B builds).  Never
-    the product."""
+    loaded with EDGEDET_LIB); extra_flags: further hipcc flags of such a variant (A/B builds); only:
+    the csrc files a variant compiles, the product's objects (build/) standing in for the rest.
+    Never the product."""
     if variant:
         diag = True
     lib = os.path.join(HERE, f"libedgedet_{variant}.so") if variant else (DIAG_LIB if diag else LIB)
@@ -92,8 +93,13 @@ def build(force=False, verbose=False, jobs=8, diag=False, variant=None, defines=
             print(r.stderr)
         return obj
 
+    def obj_of(src):
+        if variant and only and os.path.basename(src) not in only:
+            return os.path.join(HERE, "build", os.path.basename(src)[:-4] + ".o")
+        return compile_one(src)
+
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(compile_one, sources()))
+        objs = list(ex.map(obj_of, sources()))
     tmp = lib + ".tmp"
     r = subprocess.run([cc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp], capture_output=True, text=True)
     if r.returncode != 0:

@@ -598,7 +598,10 @@ class SSDLite {
     static constexpr double EPS = 1e-3;
     static constexpr int S = 320, DETS = 300, TOPK = 300;
     static constexpr double SCORE = 0.001, NMS = 0.55;
-    static constexpr int HEAD_TILE = 31;  // one x6b tile for the grouped head 1x1 convs (64 x 128)
+    // one x6b tile for the grouped head 1x1 convs: 128 x 64 (the cls heads' 546 columns fill 9 N tiles
+    // of 64 to 95 %, 5 of 128 to 85 %): the group alone 60.5 -> 51.3 us, SSD +0.8 % in alternated
+    // runs against 64 x 128 (tile 31; 128 x 128: 68.6 us, +0.5 %), profiles/r6h_head_tile_ab.txt
+    static constexpr int HEAD_TILE = 38;
 
     SSDLite(const Config& c, Packer& pk) : cfg_(c), pk_(pk), blocks_(mnv3_blocks(c.reduced_tail)) {}
 
